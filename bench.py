@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident ONC-RPC encode+decode on MI355X.
+
+BASELINE.json metric: "device-resident ONC-RPC encode+decode: Mmsgs/s and
+GiB/s vs HBM roofline". One step = one pass of the hot path over one batch:
+RpcMessage::serialise_into of every record into one send buffer
+(src/rpc_message.rs:136-164) followed by RpcMessage::try_from of every
+record of that buffer (src/rpc_message.rs:235-271), inputs resident in HBM.
+
+Workload (N=1): configs[1] — 1M Call(prog 100003, vers 4, proc 1,
+AuthNone(None) x2) with a 256 B random payload (W = 300 B on the wire),
+encode -> decode loopback. For --gpus N every rank processes its own 1M
+record shard (weak scaling, no data-path collective).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident ONC-RPC encode+decode: Mmsgs/s and GiB/s vs HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--records", type=int, default=1_000_000, help="records per GPU")
+    ap.add_argument("--payload", type=int, default=256)
+    ap.add_argument("--mode", choices=["slice", "bytes"], default="slice")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def cpu_info():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
+def cpu_baseline(hb, gpu_wire_prefix, seconds, mode):
+    """Oracle (C restatement of the reference, single thread) on a bounded
+    sample of the same workload: encode+decode round trips until `seconds`
+    of CPU work. Also checks the sample's bytes against the GPU output."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import oracle_ffi
+    import onc_rpc_amd.layout as L
+
+    chunk = 20_000
+    sub = L.HostBatch(hb.msgs[:chunk].copy(), hb.unix, hb.auth_arena, hb.payload_arena)
+    wire, off, st, _ = oracle_ffi.encode_batch(sub)
+    parity = wire == gpu_wire_prefix[: len(wire)]
+    w = np.frombuffer(wire + b"\0" * 16, np.uint8).copy()
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        wire, off, st, _ = oracle_ffi.encode_batch(sub)
+        w = np.frombuffer(wire + b"\0" * 16, np.uint8)
+        oracle_ffi.decode_batch(w, off, mode)
+        done += chunk
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    model, ncpu = cpu_info()
+    return {
+        "value": done / el / 1e6,
+        "unit": "Mmsgs/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{done} records ({chunk}-record chunks of the same configs[1] workload), "
+                  f"encode+decode round trip, {el:.1f} s on 1 thread of {ncpu}-CPU host ({model})",
+        "sample_bit_exact_vs_gpu": bool(parity),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+
+    import _onc_pkg
+
+    _onc_pkg.load()
+    import onc_rpc_amd.layout as L
+    import onc_rpc_amd.runtime as R
+    import onc_rpc_amd.shard as SH
+    import onc_rpc_amd.synth as S
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    mode = L.DECODE_BYTES if args.mode == "bytes" else L.DECODE_SLICE
+
+    n_total = args.records * world
+    lo, hi = SH.shard_bounds(n_total, world, rank)
+    n = hi - lo
+    W = 4 * 11 + args.payload                 # Call(AuthNone x2): 44 B header + payload
+    H = 44                                    # parsed header bytes per record
+    hb = S.call_none(n, args.payload, seed=1 + rank, first_xid=lo)
+    db = R.DeviceBatch.from_host(hb, dev)
+    codec = R.Codec(local_rank)
+    codec.reserve(n)
+
+    out = torch.empty(n * W + 16, dtype=torch.uint8, device=dev)
+    rec_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    enc_status = torch.empty(n, dtype=torch.int32, device=dev)
+    dec = R.DecodeBuffers(n, dev)
+
+    def step():
+        codec.encode(db, out, rec_off, enc_status)
+        codec.decode(out, rec_off, n, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # Timed region: exactly K steps, barrier + sync on both sides.
+    # Per-kernel HIP events (codec timing) bracket every launch on the
+    # codec's stream (= torch's current stream) inside the same region.
+    codec.reset_stats()
+    codec.enable_timing(True)
+    barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t_wall0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    barrier()
+    t_wall = time.perf_counter() - t_wall0
+    codec.enable_timing(False)
+    ms = ev0.elapsed_time(ev1)
+    kstats = codec.kernel_stats()
+
+    # Second, event-free pass of the same K steps (reported for comparison).
+    torch.cuda.synchronize()
+    ev2 = torch.cuda.Event(enable_timing=True)
+    ev3 = torch.cuda.Event(enable_timing=True)
+    ev2.record()
+    for _ in range(args.steps):
+        step()
+    ev3.record()
+    torch.cuda.synchronize()
+    ms_clean = ev2.elapsed_time(ev3)
+
+    t = torch.tensor([ms, ms_clean], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms_max, ms_clean_max = float(t[0]), float(t[1])
+
+    # Validation of the last step (device-side, size-independent checks).
+    ok = True
+    if int((enc_status != 0).sum()) or int((dec.status != 0).sum()):
+        ok = False
+    if int(rec_off[n]) != n * W:
+        ok = False
+    xid = dec.msgs.view(-1, 64)[:n, 0:4].contiguous().view(torch.int32).view(-1)
+    if not torch.equal(xid, (torch.arange(lo, hi, device=dev, dtype=torch.int64) & 0xFFFFFFFF).to(torch.int32)):
+        ok = False
+    okt = torch.tensor([1 if ok else 0], device=dev)
+    if dist is not None:
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    ok = bool(okt.item())
+
+    steps = args.steps
+    ms_per_step = ms_max / steps
+    value = n_total / (ms_per_step / 1e3) / 1e6       # whole-job Mmsgs/s
+    wire_gibs = n_total * W / (ms_per_step / 1e3) / 2**30
+
+    # Roofline of the dominant kernel (per-launch averages from HIP events).
+    per_rec_alg = {
+        "enc_len_kernel": 64 + 4,          # descriptor read + status write
+        "scan_tiles_kernel": 0,
+        "enc_emit_kernel": 2 * W,          # encode reads ~W, writes W
+        "decode_kernel": 2 * H + 4,        # zero-copy decode
+        "len_tiles_kernel": 4,
+        "len_apply_kernel": 12,
+    }
+    kern = {}
+    for name, (tot_ms, cnt) in kstats.items():
+        if cnt:
+            kern[name] = {"avg_us": tot_ms / cnt * 1e3, "launches": cnt,
+                          "alg_bytes_per_launch": per_rec_alg[name] * n}
+    dom = max(kern, key=lambda k: kern[k]["avg_us"])
+    d = kern[dom]
+    achieved = d["alg_bytes_per_launch"] / (d["avg_us"] * 1e-6) / 1e9
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("kernel") == dom and tj.get("records") == n:
+            traffic = tj.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "alg_bytes_per_launch": d["alg_bytes_per_launch"], "avg_launch_us": d["avg_us"]}
+    step_alg = n * (2 * W + 2 * H + 4)      # SURVEY §8(d) loopback rule (692 B/record)
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "Mmsgs/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded): Call(prog 100003, vers 4, proc 1, AuthNone(None) x2) + 256 B random payload",
+        "config": {"workload": f"configs[1]: {n // 1000}k x Call(AuthNone) {args.payload} B payload per GPU, "
+                               f"encode -> decode ({args.mode} mode) loopback, HBM-resident",
+                   "records_per_gpu": n, "wire_bytes_per_record": W, "decode_mode": args.mode,
+                   "parallelism": f"record-sharded x{world} (no collective)"},
+        "wire_GiB_per_s": wire_gibs,
+        "ms_per_step_without_kernel_events": ms_clean_max / steps,
+        "step_alg_GBs": step_alg * world / (ms_per_step / 1e3) / 1e9,
+        "roofline": roofline,
+        "kernels": kern,
+        "validated": ok,
+        "wall_s_timed_region": t_wall,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        prefix = out[: 20_000 * W].cpu().numpy().tobytes()
+        result["cpu_baseline"] = cpu_baseline(hb, prefix, args.cpu_seconds, mode)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    codec.close()
+    if dist is not None:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

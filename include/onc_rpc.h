@@ -1,0 +1,300 @@
+/*
+ * onc_rpc.h — C ABI of the MI355X (gfx950) batch ONC-RPC / XDR codec.
+ *
+ * This is the drop-in boundary for the reference crate's hot path
+ * (domodwyer/onc-rpc v0.3.3, read at /root/reference). Every entry point
+ * below names the reference interface it replaces. The reference is a Rust
+ * crate whose API is one message per call:
+ *
+ *   RpcMessage::serialise_into(&self, W: Write)  src/rpc_message.rs:136-164
+ *   RpcMessage::serialised_len(&self) -> u32      src/rpc_message.rs:201-204
+ *   RpcMessage::try_from(&[u8])                   src/rpc_message.rs:235-271
+ *   RpcMessage::try_from(Bytes)                   src/rpc_message.rs:273-314
+ *   expected_message_len(&[u8])                   src/rpc_message.rs:343-367
+ *
+ * Here the caller's per-message loop is replaced by one batch call over N
+ * independent records, executed by hand-written HIP kernels on one GPU.
+ *
+ * Conventions
+ *  - Every pointer marked [dev] is device memory (hipMalloc / torch CUDA
+ *    tensor) on the codec's device. Nothing is copied to or from the host by
+ *    these calls; all calls are asynchronous on the codec's stream.
+ *  - The caller owns every buffer (the reference never allocates on decode
+ *    and reuses caller buffers on encode, README.md:10-14). The codec only
+ *    keeps a small scratch area for the record-offset scan.
+ *  - Messages are described by fixed 64-byte descriptors (onc_msg). Opaque
+ *    bodies (auth bodies, machine names) and payloads are (offset, length)
+ *    references into caller arenas, mirroring the borrowed slices of the
+ *    reference's generic `T, P: AsRef<[u8]>` (src/call_body.rs:18-30).
+ *  - Per-record results are status codes equal to the reference's Error
+ *    variants in declaration order (src/errors.rs:6-97), plus encode-only
+ *    codes for the reference's panics and io::Errors.
+ */
+#ifndef ONC_RPC_H
+#define ONC_RPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ONC_RPC_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------ */
+/* Wire discriminants (values are the on-wire u32s)                          */
+/* ------------------------------------------------------------------------ */
+
+/* msg_type — src/rpc_message.rs:16-17 */
+#define ONC_MSG_CALL  0u
+#define ONC_MSG_REPLY 1u
+
+/* reply_stat — src/reply/reply_body.rs:11-12 */
+#define ONC_REPLY_ACCEPTED 0u
+#define ONC_REPLY_DENIED   1u
+
+/* accept_stat — src/reply/accepted_reply.rs:10-15 */
+#define ONC_ACCEPT_SUCCESS       0u
+#define ONC_ACCEPT_PROG_UNAVAIL  1u
+#define ONC_ACCEPT_PROG_MISMATCH 2u
+#define ONC_ACCEPT_PROC_UNAVAIL  3u
+#define ONC_ACCEPT_GARBAGE_ARGS  4u
+#define ONC_ACCEPT_SYSTEM_ERR    5u
+
+/* reject_stat — src/reply/rejected_reply.rs:10-11 */
+#define ONC_REJECT_RPC_MISMATCH 0u
+#define ONC_REJECT_AUTH_ERROR   1u
+
+/* auth_stat — src/reply/rejected_reply.rs:13-20 (AUTH_OK .. AUTH_FAILED = 0..7) */
+#define ONC_AUTH_STAT_MAX 7u
+
+/* Auth flavor ids — src/auth/flavor.rs:10-12 */
+#define ONC_AUTH_NONE  0u
+#define ONC_AUTH_UNIX  1u
+#define ONC_AUTH_SHORT 2u
+
+/* AuthFlavor variant (descriptor "kind") — src/auth/flavor.rs:18-49.
+ * NONE with length 0 is AuthNone(None); with length > 0 AuthNone(Some(_)).
+ * UNKNOWN writes/reads `id` as the wire discriminant. */
+#define ONC_KIND_NONE    0u
+#define ONC_KIND_UNIX    1u
+#define ONC_KIND_SHORT   2u
+#define ONC_KIND_UNKNOWN 3u
+
+/* Limits — src/auth/flavor.rs:110 (encode), :83 / opaque 200 (decode);
+ * src/auth/unix_params.rs:11-12 */
+#define ONC_MAX_AUTH_LEN         200u
+#define ONC_MAX_MACHINE_NAME_LEN 255u
+#define ONC_MAX_GIDS             16u
+
+/* Decode modes: the two reference decoders */
+#define ONC_DECODE_SLICE 0 /* TryFrom<&[u8]>  src/rpc_message.rs:235-271 */
+#define ONC_DECODE_BYTES 1 /* TryFrom<Bytes>  src/rpc_message.rs:273-314 */
+
+/* ------------------------------------------------------------------------ */
+/* Per-record status codes                                                   */
+/* ------------------------------------------------------------------------ */
+/* 1..13 are src/errors.rs:6-97 in declaration order.                        */
+#define ONC_OK                               0
+#define ONC_ERR_INCOMPLETE_MESSAGE           1  /* aux0 = buffer_len, aux1 = expected   errors.rs:14-21 */
+#define ONC_ERR_INCOMPLETE_HEADER            2  /* errors.rs:24-25 */
+#define ONC_ERR_FRAGMENTED                   3  /* errors.rs:32-33 */
+#define ONC_ERR_INVALID_MESSAGE_TYPE         4  /* aux0 = value   errors.rs:42-43 */
+#define ONC_ERR_INVALID_REPLY_TYPE           5  /* aux0 = value   errors.rs:52-53 */
+#define ONC_ERR_INVALID_REPLY_STATUS         6  /* aux0 = value   errors.rs:59-60 */
+#define ONC_ERR_INVALID_AUTH_DATA            7  /* errors.rs:63-64 */
+#define ONC_ERR_INVALID_AUTH_ERROR           8  /* aux0 = value   errors.rs:70-71 */
+#define ONC_ERR_INVALID_REJECTED_REPLY_TYPE  9  /* aux0 = value   errors.rs:77-78 */
+#define ONC_ERR_INVALID_LENGTH              10  /* errors.rs:82-83 */
+#define ONC_ERR_INVALID_RPC_VERSION         11  /* aux0 = value   errors.rs:86-87 */
+#define ONC_ERR_INVALID_MACHINE_NAME        12  /* errors.rs:91-92 — never produced by a decoder */
+#define ONC_ERR_IO_UNEXPECTED_EOF           13  /* IOError(UnexpectedEof, "failed to fill whole buffer")
+                                                   errors.rs:95-103 (slice-mode short read) */
+/* Encode-only codes (the reference panics or returns io::Error here). */
+#define ONC_ENC_TOO_LONG        100 /* io::Error InvalidInput "message length exceeds maximum"
+                                       rpc_message.rs:146-151 */
+#define ONC_ENC_AUTH_GT_200     101 /* panic: assert!(associated_data_len() <= 200) flavor.rs:110 */
+#define ONC_ENC_NAME_GT_255     102 /* panic: AuthUnixParams::new unix_params.rs:149 */
+#define ONC_ENC_GIDS_GT_16      103 /* panic: Gids::from_iter unix_params.rs:47 */
+#define ONC_ENC_BAD_DESCRIPTOR  104 /* a descriptor the Rust enums cannot represent */
+#define ONC_ENC_WRITE_ZERO      105 /* io::Error WriteZero: output capacity exhausted */
+
+/* Batch-level return codes of the API functions */
+#define ONC_RC_OK        0
+#define ONC_RC_EINVAL   -1
+#define ONC_RC_EHIP     -2
+#define ONC_RC_ENOMEM   -3
+#define ONC_RC_EALIGN   -4
+
+/* ------------------------------------------------------------------------ */
+/* Descriptors                                                               */
+/* ------------------------------------------------------------------------ */
+
+/* opaque_auth — AuthFlavor<T> (src/auth/flavor.rs:18-49). 16 bytes.
+ *  id       : wire flavor discriminant. Encode writes 0/1/2 for kinds
+ *             NONE/UNIX/SHORT and `id` for UNKNOWN; decode stores the value read.
+ *  kind_len : bits 0..23 opaque body length (NONE/SHORT/UNKNOWN),
+ *             bits 24..31 ONC_KIND_*. Unused length bits are 0 for UNIX.
+ *  ref      : NONE/SHORT/UNKNOWN: byte offset of the body in the auth arena
+ *             (decode: in the wire buffer). UNIX: index into the unix table. */
+typedef struct onc_auth {
+    uint32_t id;
+    uint32_t kind_len;
+    uint64_t ref;
+} onc_auth;
+
+#define ONC_AUTH_KIND(a)        ((uint32_t)((a).kind_len >> 24))
+#define ONC_AUTH_LEN(a)         ((uint32_t)((a).kind_len & 0xFFFFFFu))
+#define ONC_AUTH_PACK(kind, len) ((uint32_t)(((uint32_t)(kind) << 24) | ((uint32_t)(len) & 0xFFFFFFu)))
+
+/* RpcMessage<T, P> (src/rpc_message.rs:97-105) with its MessageType,
+ * CallBody (src/call_body.rs:17-30) / ReplyBody (src/reply/ *.rs). 64 bytes.
+ *
+ *  msg_type    ONC_MSG_CALL | ONC_MSG_REPLY
+ *  reply_stat  reply: ONC_REPLY_ACCEPTED | ONC_REPLY_DENIED
+ *  stat        accepted: ONC_ACCEPT_*; denied: ONC_REJECT_*
+ *  auth_stat   denied AUTH_ERROR: AuthError (0..7)
+ *  call        program / program_version / procedure (CallBody)
+ *  mismatch    low / high of ProgramMismatch or RpcVersionMismatch
+ *  payload_*   Call payload or Success payload (raw, unpadded; call_body.rs:107,
+ *              accepted_reply.rs:199): encode = payload arena offset,
+ *              decode = wire offset
+ *  cred        call credentials (unused for replies)
+ *  verf        call verifier or accepted-reply verifier */
+typedef struct onc_msg {
+    uint32_t xid;
+    uint8_t  msg_type;
+    uint8_t  reply_stat;
+    uint8_t  stat;
+    uint8_t  auth_stat;
+    union {
+        struct { uint32_t program, program_version, procedure; } call;
+        struct { uint32_t low, high, reserved; } mismatch;
+    } u;
+    uint32_t payload_len;
+    uint64_t payload_off;
+    onc_auth cred;
+    onc_auth verf;
+} onc_msg;
+
+/* AuthUnixParams<T> (src/auth/unix_params.rs:72-82). 96 bytes.
+ * name_off is an auth-arena offset (decode: wire offset). */
+typedef struct onc_unix_params {
+    uint32_t stamp;
+    uint32_t uid;
+    uint32_t gid;
+    uint32_t ngids;
+    uint64_t name_off;
+    uint32_t name_len;
+    uint32_t reserved;
+    uint32_t gids[16];
+} onc_unix_params;
+
+/* A batch of messages to encode. [dev] pointers. auth_arena and
+ * payload_arena may alias (e.g. both = the wire buffer of a decoded batch). */
+typedef struct onc_batch {
+    uint64_t               n;
+    const onc_msg*         msgs;          /* [dev] n descriptors */
+    const onc_unix_params* unix_params;   /* [dev] AUTH_UNIX table (may be NULL if unused) */
+    const uint8_t*         auth_arena;    /* [dev] auth bodies + machine names */
+    const uint8_t*         payload_arena; /* [dev] payloads */
+} onc_batch;
+
+/* Decode outputs. [dev] pointers.
+ * unix_params has 2*n slots: record i's credentials use slot 2i, its
+ * verifier slot 2i+1 (the slot index is stored in onc_auth.ref).
+ * Offsets in the decoded descriptors are wire-buffer offsets, so a decoded
+ * batch can be re-encoded with auth_arena = payload_arena = wire.
+ * For a record with status != ONC_OK the descriptor is all zero; unix slots
+ * are defined only for OK records whose auth kind is UNIX. */
+typedef struct onc_decoded {
+    onc_msg*         msgs;        /* n */
+    onc_unix_params* unix_params; /* 2n */
+    int32_t*         status;      /* n */
+    uint32_t*        aux0;        /* n: buffer_len or the offending value */
+    uint32_t*        aux1;        /* n: expected (IncompleteMessage) */
+} onc_decoded;
+
+/* ------------------------------------------------------------------------ */
+/* Codec handle                                                              */
+/* ------------------------------------------------------------------------ */
+
+typedef struct onc_codec onc_codec;
+
+/* One handle per device: a HIP stream + scan scratch. `hip_stream` may be
+ * NULL (the device's null stream) or a hipStream_t owned by the caller. */
+int onc_codec_create(onc_codec** out, int device, void* hip_stream);
+int onc_codec_destroy(onc_codec* codec);
+int onc_codec_set_stream(onc_codec* codec, void* hip_stream);
+int onc_codec_sync(onc_codec* codec);
+/* Pre-size the scan scratch for batches of up to max_records, so that later
+ * calls perform no allocation (required before capturing calls into a
+ * hipGraph; otherwise scratch grows on demand with a synchronous hipMalloc). */
+int onc_codec_reserve(onc_codec* codec, uint64_t max_records);
+/* Last HIP error string seen by this handle ("" if none). */
+const char* onc_codec_last_error(const onc_codec* codec);
+const char* onc_status_str(int32_t status);
+int onc_abi_version(void);
+
+/* Per-kernel event timing (for the bench's roofline). When enabled every
+ * kernel launch is bracketed by hipEvents on the codec stream; the
+ * accumulated device time and launch count per kernel id are returned by
+ * onc_codec_kernel_stats after a sync. Ids: see ONC_K_*. */
+#define ONC_K_ENC_LEN     0
+#define ONC_K_SCAN_TILES  1
+#define ONC_K_ENC_EMIT    2
+#define ONC_K_DEC_PARSE   3
+#define ONC_K_LEN_TILES   4
+#define ONC_K_LEN_APPLY   5
+#define ONC_K_COUNT       6
+int onc_codec_enable_timing(onc_codec* codec, int enable);
+int onc_codec_kernel_stats(onc_codec* codec, double* ms_total /*[ONC_K_COUNT]*/,
+                           uint64_t* launches /*[ONC_K_COUNT]*/);
+int onc_codec_reset_stats(onc_codec* codec);
+const char* onc_kernel_name(int kernel_id);
+
+/* ------------------------------------------------------------------------ */
+/* Encode — RpcMessage::serialise_into (src/rpc_message.rs:136-164)          */
+/* ------------------------------------------------------------------------ */
+
+/* serialised_len() of every record (src/rpc_message.rs:201-204) plus the
+ * encode-time validation of serialise_into (oversize, panics).
+ * rec_len[dev,n] receives the length (0 for a record whose status != OK);
+ * status[dev,n] receives ONC_OK or an ONC_ENC_* code. */
+int onc_encode_lengths(onc_codec* codec, const onc_batch* batch,
+                       uint32_t* rec_len, int32_t* status);
+
+/* Encode every record back to back into out[dev] (16-byte aligned,
+ * out_cap bytes): the batch equivalent of calling serialise_into for each
+ * message in order on one Cursor<Vec<u8>> (a TCP send buffer).
+ *   rec_off[dev, n+1]: record i occupies [rec_off[i], rec_off[i+1]);
+ *                      rec_off[n] is the total byte count.
+ *   status[dev, n]   : ONC_OK or ONC_ENC_*. Records that fail validation
+ *                      occupy 0 bytes. Bytes at or beyond out_cap are never
+ *                      written; records ending beyond it get ONC_ENC_WRITE_ZERO.
+ *   rec_len[dev, n]  : optional (may be NULL) serialised lengths. */
+int onc_encode(onc_codec* codec, const onc_batch* batch,
+               uint8_t* out, uint64_t out_cap,
+               uint64_t* rec_off, int32_t* status, uint32_t* rec_len);
+
+/* ------------------------------------------------------------------------ */
+/* Decode — RpcMessage::try_from(&[u8]) / try_from(Bytes)                    */
+/* ------------------------------------------------------------------------ */
+
+/* Decode record i = wire[rec_off[i] .. rec_off[i+1]) for i < n, each
+ * exactly as the reference decodes one buffer that must hold exactly one
+ * message (src/rpc_message.rs:238-242). mode = ONC_DECODE_SLICE | _BYTES. */
+int onc_decode(onc_codec* codec, const uint8_t* wire, const uint64_t* rec_off,
+               uint64_t n, int mode, const onc_decoded* out);
+
+/* Exclusive scan of record lengths into offsets:
+ * rec_off[0] = base, rec_off[i+1] = rec_off[i] + rec_len[i]  ([dev]). */
+int onc_scan_lengths(onc_codec* codec, const uint32_t* rec_len, uint64_t n,
+                     uint64_t base, uint64_t* rec_off);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* ONC_RPC_H */

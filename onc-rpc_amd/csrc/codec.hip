@@ -1,0 +1,330 @@
+// codec.hip — the C ABI (include/onc_rpc.h) over the gfx950 kernels.
+//
+// A codec handle = one device + one HIP stream + scan scratch. Every call
+// only enqueues work on the handle's stream; no host<->device copies and no
+// synchronisation happen inside encode/decode (the caller syncs).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+struct onc_codec {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint64_t* scratch = nullptr;   // [tile_sum | tile_base], 2 * scratch_tiles entries
+    uint64_t scratch_tiles = 0;
+    bool timing = false;
+    struct Pending {
+        int kernel;
+        hipEvent_t start, stop;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> spare;
+    double ms[ONC_K_COUNT] = {};
+    uint64_t launches[ONC_K_COUNT] = {};
+    std::string last_error;
+};
+
+namespace {
+
+int fail(onc_codec* c, hipError_t e, const char* what) {
+    if (c) {
+        c->last_error = std::string(what) + ": " + hipGetErrorString(e);
+    }
+    return ONC_RC_EHIP;
+}
+
+hipEvent_t take_event(onc_codec* c) {
+    if (!c->spare.empty()) {
+        hipEvent_t e = c->spare.back();
+        c->spare.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// Launch one kernel, bracketed by events when timing is on.
+template <class F>
+int run(onc_codec* c, int kernel, const char* what, F&& launch) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (c->timing) {
+        a = take_event(c);
+        b = take_event(c);
+        if (a) hipEventRecord(a, c->stream);
+    }
+    const hipError_t e = launch();
+    if (c->timing && a && b) {
+        hipEventRecord(b, c->stream);
+        c->pending.push_back({kernel, a, b});
+    }
+    if (e != hipSuccess) return fail(c, e, what);
+    return ONC_RC_OK;
+}
+
+int ensure_scratch(onc_codec* c, uint64_t tiles) {
+    if (tiles <= c->scratch_tiles) return ONC_RC_OK;
+    uint64_t want = c->scratch_tiles ? c->scratch_tiles : 1024;
+    while (want < tiles) want *= 2;
+    if (c->scratch) {
+        // The stream may still be using the old scratch.
+        hipStreamSynchronize(c->stream);
+        hipFree(c->scratch);
+        c->scratch = nullptr;
+        c->scratch_tiles = 0;
+    }
+    hipError_t e = hipMalloc(&c->scratch, 2 * want * sizeof(uint64_t));
+    if (e != hipSuccess) {
+        fail(c, e, "hipMalloc(scratch)");
+        return ONC_RC_ENOMEM;
+    }
+    c->scratch_tiles = want;
+    return ONC_RC_OK;
+}
+
+int set_device(onc_codec* c) {
+    const hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) return fail(c, e, "hipSetDevice");
+    return ONC_RC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int onc_abi_version(void) { return ONC_RPC_ABI_VERSION; }
+
+int onc_codec_create(onc_codec** out, int device, void* hip_stream) {
+    if (!out) return ONC_RC_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return ONC_RC_EINVAL;
+    onc_codec* c = new onc_codec();
+    c->device = device;
+    c->stream = static_cast<hipStream_t>(hip_stream);
+    if (set_device(c) != ONC_RC_OK) {
+        delete c;
+        return ONC_RC_EHIP;
+    }
+    *out = c;
+    return ONC_RC_OK;
+}
+
+int onc_codec_destroy(onc_codec* c) {
+    if (!c) return ONC_RC_EINVAL;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    for (auto& p : c->pending) {
+        hipEventDestroy(p.start);
+        hipEventDestroy(p.stop);
+    }
+    for (auto e : c->spare) hipEventDestroy(e);
+    if (c->scratch) hipFree(c->scratch);
+    delete c;
+    return ONC_RC_OK;
+}
+
+int onc_codec_set_stream(onc_codec* c, void* hip_stream) {
+    if (!c) return ONC_RC_EINVAL;
+    c->stream = static_cast<hipStream_t>(hip_stream);
+    return ONC_RC_OK;
+}
+
+int onc_codec_sync(onc_codec* c) {
+    if (!c) return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return fail(c, e, "hipStreamSynchronize");
+    return ONC_RC_OK;
+}
+
+int onc_codec_reserve(onc_codec* c, uint64_t max_records) {
+    if (!c) return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    return ensure_scratch(c, onc::num_tiles(max_records));
+}
+
+const char* onc_codec_last_error(const onc_codec* c) { return c ? c->last_error.c_str() : "null codec"; }
+
+const char* onc_status_str(int32_t s) {
+    switch (s) {
+        case ONC_OK: return "ok";
+        case ONC_ERR_INCOMPLETE_MESSAGE: return "incomplete rpc message";
+        case ONC_ERR_INCOMPLETE_HEADER: return "incomplete fragment header";
+        case ONC_ERR_FRAGMENTED: return "RPC message is fragmented";
+        case ONC_ERR_INVALID_MESSAGE_TYPE: return "invalid rpc message type";
+        case ONC_ERR_INVALID_REPLY_TYPE: return "invalid rpc reply type";
+        case ONC_ERR_INVALID_REPLY_STATUS: return "invalid rpc reply status";
+        case ONC_ERR_INVALID_AUTH_DATA: return "invalid rpc auth data";
+        case ONC_ERR_INVALID_AUTH_ERROR: return "invalid rpc auth error status";
+        case ONC_ERR_INVALID_REJECTED_REPLY_TYPE: return "invalid rpc rejected reply type";
+        case ONC_ERR_INVALID_LENGTH: return "invalid length in rpc message";
+        case ONC_ERR_INVALID_RPC_VERSION: return "invalid rpc version";
+        case ONC_ERR_INVALID_MACHINE_NAME: return "invalid machine name";
+        case ONC_ERR_IO_UNEXPECTED_EOF: return "i/o error (UnexpectedEof): failed to fill whole buffer";
+        case ONC_ENC_TOO_LONG: return "message length exceeds maximum";
+        case ONC_ENC_AUTH_GT_200: return "auth associated data exceeds 200 bytes";
+        case ONC_ENC_NAME_GT_255: return "machine name exceeds 255 bytes";
+        case ONC_ENC_GIDS_GT_16: return "more than 16 gids";
+        case ONC_ENC_BAD_DESCRIPTOR: return "invalid message descriptor";
+        case ONC_ENC_WRITE_ZERO: return "failed to write whole buffer";
+        default: return "unknown status";
+    }
+}
+
+const char* onc_kernel_name(int k) {
+    switch (k) {
+        case ONC_K_ENC_LEN: return "enc_len_kernel";
+        case ONC_K_SCAN_TILES: return "scan_tiles_kernel";
+        case ONC_K_ENC_EMIT: return "enc_emit_kernel";
+        case ONC_K_DEC_PARSE: return "decode_kernel";
+        case ONC_K_LEN_TILES: return "len_tiles_kernel";
+        case ONC_K_LEN_APPLY: return "len_apply_kernel";
+        default: return "?";
+    }
+}
+
+int onc_codec_enable_timing(onc_codec* c, int enable) {
+    if (!c) return ONC_RC_EINVAL;
+    c->timing = enable != 0;
+    return ONC_RC_OK;
+}
+
+int onc_codec_kernel_stats(onc_codec* c, double* ms_total, uint64_t* launches) {
+    if (!c) return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return fail(c, e, "hipStreamSynchronize");
+    for (auto& p : c->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.start, p.stop) == hipSuccess) {
+            c->ms[p.kernel] += ms;
+            c->launches[p.kernel] += 1;
+        }
+        c->spare.push_back(p.start);
+        c->spare.push_back(p.stop);
+    }
+    c->pending.clear();
+    for (int k = 0; k < ONC_K_COUNT; ++k) {
+        if (ms_total) ms_total[k] = c->ms[k];
+        if (launches) launches[k] = c->launches[k];
+    }
+    return ONC_RC_OK;
+}
+
+int onc_codec_reset_stats(onc_codec* c) {
+    if (!c) return ONC_RC_EINVAL;
+    double tmp[ONC_K_COUNT];
+    uint64_t tl[ONC_K_COUNT];
+    const int rc = onc_codec_kernel_stats(c, tmp, tl);
+    for (int k = 0; k < ONC_K_COUNT; ++k) {
+        c->ms[k] = 0;
+        c->launches[k] = 0;
+    }
+    return rc;
+}
+
+static int check_batch(const onc_batch* b) {
+    if (!b) return ONC_RC_EINVAL;
+    if (b->n && !b->msgs) return ONC_RC_EINVAL;
+    return ONC_RC_OK;
+}
+
+int onc_encode_lengths(onc_codec* c, const onc_batch* batch, uint32_t* rec_len, int32_t* status) {
+    if (!c || check_batch(batch) != ONC_RC_OK || (batch->n && (!rec_len || !status))) return ONC_RC_EINVAL;
+    if (batch->n == 0) return ONC_RC_OK;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    const uint64_t tiles = onc::num_tiles(batch->n);
+    int rc = ensure_scratch(c, tiles);
+    if (rc != ONC_RC_OK) return rc;
+    onc::EncArgs a{};
+    a.n = batch->n;
+    a.msgs = batch->msgs;
+    a.unix = batch->unix_params;
+    a.auth_arena = batch->auth_arena;
+    a.payload_arena = batch->payload_arena;
+    a.status = status;
+    a.rec_len = rec_len;
+    a.tile_sum = c->scratch;
+    return run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
+}
+
+int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
+               int32_t* status, uint32_t* rec_len) {
+    if (!c || check_batch(batch) != ONC_RC_OK || !rec_off) return ONC_RC_EINVAL;
+    if (batch->n && (!status || (!out && out_cap))) return ONC_RC_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(out) & 15) != 0) return ONC_RC_EALIGN;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    if (batch->n == 0) {
+        const hipError_t e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
+        return e == hipSuccess ? ONC_RC_OK : fail(c, e, "hipMemsetAsync");
+    }
+    const uint64_t tiles = onc::num_tiles(batch->n);
+    int rc = ensure_scratch(c, tiles);
+    if (rc != ONC_RC_OK) return rc;
+    onc::EncArgs a{};
+    a.n = batch->n;
+    a.msgs = batch->msgs;
+    a.unix = batch->unix_params;
+    a.auth_arena = batch->auth_arena;
+    a.payload_arena = batch->payload_arena;
+    a.out = out;
+    a.out_cap = out ? out_cap : 0;
+    a.rec_off = rec_off;
+    a.status = status;
+    a.rec_len = rec_len;
+    a.tile_sum = c->scratch;
+    a.tile_base = c->scratch + c->scratch_tiles;
+    rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    rc = run(c, ONC_K_SCAN_TILES, "scan_tiles", [&] {
+        return onc::launch_scan_tiles(a.tile_sum, c->scratch + c->scratch_tiles, tiles, 0, rec_off + batch->n,
+                                      c->stream);
+    });
+    if (rc != ONC_RC_OK) return rc;
+    return run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
+}
+
+int onc_decode(onc_codec* c, const uint8_t* wire, const uint64_t* rec_off, uint64_t n, int mode,
+               const onc_decoded* out) {
+    if (!c || !out || (mode != ONC_DECODE_SLICE && mode != ONC_DECODE_BYTES)) return ONC_RC_EINVAL;
+    if (n == 0) return ONC_RC_OK;
+    if (!rec_off || !out->msgs || !out->unix_params || !out->status || !out->aux0 || !out->aux1)
+        return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    onc::DecArgs a{};
+    a.n = n;
+    a.wire = wire;
+    a.rec_off = rec_off;
+    a.out = *out;
+    return run(c, ONC_K_DEC_PARSE, "decode", [&] { return onc::launch_decode(a, mode, c->stream); });
+}
+
+int onc_scan_lengths(onc_codec* c, const uint32_t* rec_len, uint64_t n, uint64_t base, uint64_t* rec_off) {
+    if (!c || !rec_off || (n && !rec_len)) return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    if (n == 0) {
+        const hipError_t e = hipMemcpyAsync(rec_off, &base, sizeof(base), hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) return fail(c, e, "hipMemcpyAsync");
+        return onc_codec_sync(c);   // `base` lives on this stack frame
+    }
+    const uint64_t tiles = onc::num_tiles(n);
+    int rc = ensure_scratch(c, tiles);
+    if (rc != ONC_RC_OK) return rc;
+    uint64_t* tile_sum = c->scratch;
+    uint64_t* tile_base = c->scratch + c->scratch_tiles;
+    rc = run(c, ONC_K_LEN_TILES, "len_tiles", [&] { return onc::launch_len_tiles(rec_len, n, tile_sum, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    rc = run(c, ONC_K_SCAN_TILES, "scan_tiles",
+             [&] { return onc::launch_scan_tiles(tile_sum, tile_base, tiles, base, rec_off + n, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    return run(c, ONC_K_LEN_APPLY, "len_apply",
+               [&] { return onc::launch_len_apply(rec_len, n, tile_base, rec_off, c->stream); });
+}
+
+}  // extern "C"

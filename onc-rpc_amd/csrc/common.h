@@ -1,0 +1,273 @@
+// common.h — device-side building blocks shared by the gfx950 codec kernels.
+//
+// Everything here is integer/byte work on 64-wide wavefronts. The wire is a
+// byte stream of big-endian u32 words and raw payload bytes; registers hold
+// stream bytes in little-endian order (stream byte b of a word = register
+// byte b), so a header field value v is stored as __builtin_bswap32(v).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/onc_rpc.h"
+
+namespace onc {
+
+constexpr int kTile = 256;        // records per tile (= threads per block)
+constexpr int kScanThreads = 1024;
+
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+// Bytes [sh, sh+4) of the 8-byte little-endian concatenation lo|hi
+// (v_alignbyte_b32).
+__device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh) {
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+// pad_length — reference src/opaque.rs:115-121
+__host__ __device__ __forceinline__ uint32_t pad4(uint32_t l) { return (4u - (l & 3u)) & 3u; }
+__host__ __device__ __forceinline__ uint32_t words4(uint32_t l) { return (l + 3u) >> 2; }
+
+// Four stream bytes at absolute byte address `addr`, bytes at or beyond
+// `lim` read as zero. Precondition: addr < lim. Only aligned dwords that
+// contain at least one byte < lim are touched, so the read never leaves
+// the valid range's pages.
+__device__ __forceinline__ uint32_t load4_masked(uintptr_t addr, uintptr_t lim) {
+    const uintptr_t al = addr & ~uintptr_t(3);
+    const uint32_t sh = uint32_t(addr & 3);
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(al);
+    const uint32_t w0 = p[0];
+    const uint32_t w1 = (sh != 0 && al + 4 < lim) ? p[1] : 0u;
+    uint32_t v = funnel(w0, w1, sh);
+    const uintptr_t n = lim - addr;
+    if (n < 4) v &= (1u << (8u * uint32_t(n))) - 1u;
+    return v;
+}
+
+// Same without the tail mask: all four bytes are known to be valid.
+__device__ __forceinline__ uint32_t load4(uintptr_t addr) {
+    const uintptr_t al = addr & ~uintptr_t(3);
+    const uint32_t sh = uint32_t(addr & 3);
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(al);
+    const uint32_t w0 = p[0];
+    const uint32_t w1 = sh ? p[1] : 0u;
+    return funnel(w0, w1, sh);
+}
+
+// ---------------------------------------------------------------------------
+// Encode planning: serialised_len + validation of one descriptor
+// ---------------------------------------------------------------------------
+//
+// Word counts of the header part of a record (everything before the raw
+// payload). XDR pads every item to 4 bytes, so the header is a whole number
+// of words relative to the record start; only the payload is unpadded and it
+// always comes last (call_body.rs:107, accepted_reply.rs:199).
+
+struct AuthPlan {
+    uint32_t words;    // serialised_len / 4  (flavor.rs:154-174)
+    uint32_t assoc;    // associated_data_len  (flavor.rs:142-150)
+    int32_t status;    // construction-time panics
+};
+
+__device__ __forceinline__ AuthPlan plan_auth(const onc_auth& a, const onc_unix_params* unix) {
+    AuthPlan p;
+    const uint32_t kind = a.kind_len >> 24;
+    const uint32_t len = a.kind_len & 0xFFFFFFu;
+    p.status = ONC_OK;
+    if (kind == ONC_KIND_UNIX) {
+        const onc_unix_params* u = unix + a.ref;
+        const uint32_t nl = u->name_len, ng = u->ngids;
+        // AuthUnixParams::new panics (unix_params.rs:149), then Gids (:47)
+        if (nl > ONC_MAX_MACHINE_NAME_LEN) { p.status = ONC_ENC_NAME_GT_255; p.words = 0; p.assoc = 0; return p; }
+        if (ng > ONC_MAX_GIDS) { p.status = ONC_ENC_GIDS_GT_16; p.words = 0; p.assoc = 0; return p; }
+        // id + len + stamp + opaque(name) + uid + gid + ngids + gids
+        p.words = 2 + 1 + 1 + words4(nl) + 3 + ng;
+        p.assoc = 12 + nl + 4 * ng;               // unix_params.rs:234-245
+    } else if (kind <= ONC_KIND_UNKNOWN) {
+        p.words = 2 + words4(len);                // id + opaque
+        p.assoc = len;
+    } else {
+        p.status = ONC_ENC_BAD_DESCRIPTOR; p.words = 0; p.assoc = 0;
+    }
+    return p;
+}
+
+// meta word: cred words | verf words << 8 | header words << 16
+struct RecPlan {
+    uint64_t len;     // serialised_len (0 if status != OK)
+    uint32_t meta;
+    int32_t status;
+};
+
+__device__ __forceinline__ uint32_t meta_cw(uint32_t m) { return m & 0xFFu; }
+__device__ __forceinline__ uint32_t meta_vw(uint32_t m) { return (m >> 8) & 0xFFu; }
+__device__ __forceinline__ uint32_t meta_hw(uint32_t m) { return m >> 16; }
+
+// RpcMessage::serialised_len (rpc_message.rs:201-204) plus the checks of
+// serialise_into in reference order: descriptor / construction panics
+// (cred, then verf), oversize (rpc_message.rs:146-151), then the
+// associated-data assert (flavor.rs:110, cred before verf).
+__device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_params* unix) {
+    RecPlan r;
+    r.len = 0;
+    r.meta = 0;
+    r.status = ONC_OK;
+    uint32_t cw = 0, vw = 0, hw;
+    uint64_t body = 0;
+    uint32_t assoc_c = 0, assoc_v = 0;
+    if (d.msg_type == ONC_MSG_CALL) {
+        AuthPlan c = plan_auth(d.cred, unix);
+        if (c.status) { r.status = c.status; return r; }
+        AuthPlan v = plan_auth(d.verf, unix);
+        if (v.status) { r.status = v.status; return r; }
+        cw = c.words; vw = v.words;
+        assoc_c = c.assoc; assoc_v = v.assoc;
+        hw = 7 + cw + vw;   // mark, xid, mtype, rpcvers, prog, vers, proc
+        body = d.payload_len;
+    } else if (d.msg_type == ONC_MSG_REPLY) {
+        if (d.reply_stat == ONC_REPLY_ACCEPTED) {
+            if (d.stat > ONC_ACCEPT_SYSTEM_ERR) { r.status = ONC_ENC_BAD_DESCRIPTOR; return r; }
+            AuthPlan v = plan_auth(d.verf, unix);
+            if (v.status) { r.status = v.status; return r; }
+            vw = v.words; assoc_v = v.assoc;
+            // mark, xid, mtype, reply_stat, verf, accept_stat [, low, high]
+            hw = 4 + vw + 1 + (d.stat == ONC_ACCEPT_PROG_MISMATCH ? 2 : 0);
+            body = d.stat == ONC_ACCEPT_SUCCESS ? d.payload_len : 0;
+        } else if (d.reply_stat == ONC_REPLY_DENIED) {
+            if (d.stat > ONC_REJECT_AUTH_ERROR) { r.status = ONC_ENC_BAD_DESCRIPTOR; return r; }
+            if (d.stat == ONC_REJECT_AUTH_ERROR && d.auth_stat > ONC_AUTH_STAT_MAX) {
+                r.status = ONC_ENC_BAD_DESCRIPTOR; return r;
+            }
+            hw = 5 + (d.stat == ONC_REJECT_RPC_MISMATCH ? 2 : 1);
+        } else {
+            r.status = ONC_ENC_BAD_DESCRIPTOR; return r;
+        }
+    } else {
+        r.status = ONC_ENC_BAD_DESCRIPTOR; return r;
+    }
+    const uint64_t total = 4ull * hw + body;
+    if (total & 0xFFFFFFFF80000000ull) { r.status = ONC_ENC_TOO_LONG; return r; }
+    if (assoc_c > ONC_MAX_AUTH_LEN || assoc_v > ONC_MAX_AUTH_LEN) { r.status = ONC_ENC_AUTH_GT_200; return r; }
+    r.len = total;
+    r.meta = cw | (vw << 8) | (hw << 16);
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// Encode word generator: stream word k of a planned record
+// ---------------------------------------------------------------------------
+
+struct EncSrc {
+    const onc_unix_params* unix;
+    uintptr_t auth_arena;
+    uintptr_t payload_arena;
+};
+
+// Word j of an opaque_auth (flavor.rs:106-129): id, length, body words
+// (last one zero padded, opaque.rs:38-56) or the AUTH_UNIX params
+// (unix_params.rs:162-176).
+__device__ __forceinline__ uint32_t auth_word(const onc_auth& a, uint32_t j, const EncSrc& s) {
+    const uint32_t kind = a.kind_len >> 24;
+    if (j == 0) {
+        const uint32_t id = kind == ONC_KIND_UNKNOWN ? a.id : kind;
+        return bswap(id);
+    }
+    if (kind != ONC_KIND_UNIX) {
+        const uint32_t len = a.kind_len & 0xFFFFFFu;
+        if (j == 1) return bswap(len);
+        const uintptr_t b = s.auth_arena + a.ref;
+        return load4_masked(b + 4ull * (j - 2), b + len);
+    }
+    const onc_unix_params* u = s.unix + a.ref;
+    const uint32_t nl = u->name_len, nw = words4(nl), ng = u->ngids;
+    if (j == 1) return bswap(20u + 4u * nw + 4u * ng);    // AuthUnixParams::serialised_len
+    if (j == 2) return bswap(u->stamp);
+    if (j == 3) return bswap(nl);
+    j -= 4;
+    if (j < nw) {
+        const uintptr_t b = s.auth_arena + u->name_off;
+        return load4_masked(b + 4ull * j, b + nl);
+    }
+    j -= nw;
+    if (j == 0) return bswap(u->uid);
+    if (j == 1) return bswap(u->gid);
+    if (j == 2) return bswap(ng);
+    return bswap(u->gids[j - 3]);
+}
+
+// Header word k < hw of record (d, len, meta).
+__device__ __forceinline__ uint32_t header_word(const onc_msg& d, uint32_t len, uint32_t meta, uint32_t k,
+                                                const EncSrc& s) {
+    if (k == 0) return bswap((len - 4u) | 0x80000000u);   // rpc_message.rs:156
+    if (k == 1) return bswap(d.xid);
+    if (k == 2) return bswap(uint32_t(d.msg_type));
+    if (d.msg_type == ONC_MSG_CALL) {
+        if (k == 3) return bswap(2u);                      // RPC_VERSION call_body.rs:10
+        if (k == 4) return bswap(d.u.call.program);
+        if (k == 5) return bswap(d.u.call.program_version);
+        if (k == 6) return bswap(d.u.call.procedure);
+        k -= 7;
+        const uint32_t cw = meta_cw(meta);
+        if (k < cw) return auth_word(d.cred, k, s);
+        return auth_word(d.verf, k - cw, s);
+    }
+    if (k == 3) return bswap(uint32_t(d.reply_stat));
+    if (d.reply_stat == ONC_REPLY_ACCEPTED) {
+        k -= 4;
+        const uint32_t vw = meta_vw(meta);
+        if (k < vw) return auth_word(d.verf, k, s);
+        k -= vw;
+        if (k == 0) return bswap(uint32_t(d.stat));
+        if (k == 1) return bswap(d.u.mismatch.low);
+        return bswap(d.u.mismatch.high);
+    }
+    if (k == 4) return bswap(uint32_t(d.stat));
+    if (d.stat == ONC_REJECT_RPC_MISMATCH) return bswap(k == 5 ? d.u.mismatch.low : d.u.mismatch.high);
+    return bswap(uint32_t(d.auth_stat));
+}
+
+// Stream word k (any integer) of the record; zero outside [0, len).
+__device__ __forceinline__ uint32_t record_word(const onc_msg& d, uint32_t len, uint32_t meta, int64_t k,
+                                                const EncSrc& s) {
+    if (k < 0 || 4 * k >= int64_t(len)) return 0u;
+    const uint32_t hw = meta_hw(meta);
+    if (uint64_t(k) < hw) return header_word(d, len, meta, uint32_t(k), s);
+    const uint64_t j = uint64_t(k) - hw;
+    const uintptr_t b = s.payload_arena + d.payload_off;
+    return load4_masked(b + 4 * j, b + d.payload_len);
+}
+
+// ---------------------------------------------------------------------------
+// Block-wide exclusive scan of u64 over 256 threads (4 waves)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+// Returns the exclusive prefix of v within the block; *total = block sum.
+template <int NT>
+__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* s_wave, uint64_t* total) {
+    constexpr int NW = NT / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t incl = wave_incl_scan_u64(v);
+    if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    uint64_t wave_base = 0, sum = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        const uint64_t t = s_wave[w];
+        if (w < wave) wave_base += t;
+        sum += t;
+    }
+    *total = sum;
+    __syncthreads();   // s_wave may be reused by the caller
+    return wave_base + incl - v;
+}
+
+}  // namespace onc

@@ -1,0 +1,297 @@
+// decode.hip — batch RpcMessage::try_from for gfx950.
+//
+// Reference decoders, one message per buffer:
+//   slice mode  RpcMessage::try_from(&[u8])  src/rpc_message.rs:235-271
+//   Bytes mode  RpcMessage::try_from(Bytes)  src/rpc_message.rs:273-314
+// with the reader chains of call_body.rs:37-69 / :181-209,
+// auth/flavor.rs:52-94 / :190-222, auth/unix_params.rs:90-129 / :252-276,
+// opaque.rs:72-98, bytes_ext.rs:17-42 and reply/*.
+//
+// One lane per record runs the reference's recursive descent as a flat
+// state machine over the record's bytes [rec_off[i], rec_off[i+1]). The
+// decode is zero-copy like the reference: opaque bodies and payloads are
+// returned as (wire offset, length), never moved. The first error wins, in
+// the reference's check order, per mode; the two modes differ only where
+// the reference does (short reads: IOError vs InvalidLength; AUTH_UNIX is
+// parsed inside its length-bounded slice in Bytes mode).
+#include "common.h"
+#include "kernels.h"
+
+namespace onc {
+
+// Big-endian u32 at record-relative position pos (all 4 bytes valid).
+#define ONC_RD(var)                                   \
+    do {                                              \
+        if (pos + 4u > end) return kShort;            \
+        var = bswap(load4(base + pos));               \
+        pos += 4u;                                    \
+    } while (0)
+
+template <int MODE>
+struct Rules {
+    // Short read: Cursor::read_exact -> IOError(UnexpectedEof) (errors.rs:99-103)
+    // vs BytesReaderExt::try_u32 -> InvalidLength (bytes_ext.rs:18-20).
+    static constexpr int32_t kShort = MODE == ONC_DECODE_BYTES ? ONC_ERR_INVALID_LENGTH : ONC_ERR_IO_UNEXPECTED_EOF;
+};
+
+// Slice mode AuthFlavor::from_cursor (flavor.rs:52-94) with
+// AuthUnixParams::from_cursor (unix_params.rs:90-129) and
+// Opaque::from_wire (opaque.rs:72-98; bound = the whole message, `end`).
+__device__ __forceinline__ int32_t auth_slice(uintptr_t base, uint32_t& pos, uint32_t end, uint64_t rec_off,
+                                              uint64_t slot, onc_auth& a, onc_unix_params* uo) {
+    constexpr int32_t kShort = Rules<ONC_DECODE_SLICE>::kShort;
+    uint32_t fl;
+    ONC_RD(fl);
+    a.id = fl;
+    if (fl == ONC_AUTH_UNIX) {
+        uint32_t n;
+        ONC_RD(n);
+        if (n > ONC_MAX_AUTH_LEN) return ONC_ERR_INVALID_LENGTH;           // flavor.rs:83-85
+        const uint32_t start = pos;
+        onc_unix_params* u = uo + slot;
+        uint32_t stamp, nl, uid, gid, ng;
+        ONC_RD(stamp);
+        ONC_RD(nl);
+        if (nl > ONC_MAX_MACHINE_NAME_LEN) return ONC_ERR_INVALID_LENGTH;   // opaque.rs:77-79
+        if (uint64_t(pos) + nl + pad4(nl) > end) return ONC_ERR_INVALID_LENGTH;  // opaque.rs:87-90
+        const uint32_t name_pos = pos;
+        pos += nl + pad4(nl);
+        ONC_RD(uid);
+        ONC_RD(gid);
+        ONC_RD(ng);
+        if (ng > ONC_MAX_GIDS) return ONC_ERR_INVALID_AUTH_DATA;          // unix_params.rs:112
+        for (uint32_t g = 0; g < ONC_MAX_GIDS; ++g) {
+            uint32_t v = 0;
+            if (g < ng) ONC_RD(v);
+            u->gids[g] = v;
+        }
+        if (pos - start != n) return ONC_ERR_INVALID_AUTH_DATA;          // unix_params.rs:117-119
+        u->stamp = stamp;
+        u->uid = uid;
+        u->gid = gid;
+        u->ngids = ng;
+        u->name_off = rec_off + name_pos;
+        u->name_len = nl;
+        u->reserved = 0;
+        a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
+        a.ref = slot;
+        return ONC_OK;
+    }
+    uint32_t n;
+    ONC_RD(n);
+    if (n > ONC_MAX_AUTH_LEN) return ONC_ERR_INVALID_LENGTH;
+    if (uint64_t(pos) + n + pad4(n) > end) return ONC_ERR_INVALID_LENGTH;
+    const uint32_t kind = fl == ONC_AUTH_NONE ? ONC_KIND_NONE : (fl == ONC_AUTH_SHORT ? ONC_KIND_SHORT : ONC_KIND_UNKNOWN);
+    a.kind_len = ONC_AUTH_PACK(kind, n);
+    a.ref = rec_off + pos;
+    pos += n + pad4(n);
+    return ONC_OK;
+}
+
+// Bytes mode AuthFlavor::try_from(Bytes) (flavor.rs:190-222): the body is
+// first cut with try_array(200) (bytes_ext.rs:25-42); AUTH_UNIX is parsed
+// inside that slice (unix_params.rs:252-276) and must fill it exactly.
+__device__ __forceinline__ int32_t auth_bytes(uintptr_t base, uint32_t& pos, uint32_t end, uint64_t rec_off,
+                                              uint64_t slot, onc_auth& a, onc_unix_params* uo) {
+    constexpr int32_t kShort = Rules<ONC_DECODE_BYTES>::kShort;
+    uint32_t fl, n;
+    ONC_RD(fl);
+    ONC_RD(n);
+    if (n > ONC_MAX_AUTH_LEN) return ONC_ERR_INVALID_LENGTH;
+    if (uint64_t(n) + pad4(n) > end - pos) return ONC_ERR_INVALID_LENGTH;
+    const uint32_t bstart = pos, bend = pos + n;
+    pos += n + pad4(n);
+    a.id = fl;
+    if (fl == ONC_AUTH_UNIX) {
+        onc_unix_params* u = uo + slot;
+        uint32_t q = bstart;
+        uint32_t stamp, nl, uid, gid, ng;
+#define ONC_RDQ(var)                                           \
+    do {                                                       \
+        if (q + 4u > bend) return ONC_ERR_INVALID_LENGTH;      \
+        var = bswap(load4(base + q));                          \
+        q += 4u;                                               \
+    } while (0)
+        ONC_RDQ(stamp);
+        ONC_RDQ(nl);
+        if (nl > ONC_MAX_MACHINE_NAME_LEN) return ONC_ERR_INVALID_LENGTH;
+        if (uint64_t(nl) + pad4(nl) > bend - q) return ONC_ERR_INVALID_LENGTH;
+        const uint32_t name_pos = q;
+        q += nl + pad4(nl);
+        ONC_RDQ(uid);
+        ONC_RDQ(gid);
+        ONC_RDQ(ng);
+        if (ng > ONC_MAX_GIDS) return ONC_ERR_INVALID_AUTH_DATA;
+        for (uint32_t g = 0; g < ONC_MAX_GIDS; ++g) {
+            uint32_t v = 0;
+            if (g < ng) ONC_RDQ(v);
+            u->gids[g] = v;
+        }
+#undef ONC_RDQ
+        // params.serialised_len() != auth_data.len() -> InvalidAuthData (flavor.rs:204-208)
+        if (20u + nl + pad4(nl) + 4u * ng != n) return ONC_ERR_INVALID_AUTH_DATA;
+        u->stamp = stamp;
+        u->uid = uid;
+        u->gid = gid;
+        u->ngids = ng;
+        u->name_off = rec_off + name_pos;
+        u->name_len = nl;
+        u->reserved = 0;
+        a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
+        a.ref = slot;
+        return ONC_OK;
+    }
+    const uint32_t kind = fl == ONC_AUTH_NONE ? ONC_KIND_NONE : (fl == ONC_AUTH_SHORT ? ONC_KIND_SHORT : ONC_KIND_UNKNOWN);
+    a.kind_len = ONC_AUTH_PACK(kind, n);
+    a.ref = rec_off + bstart;
+    return ONC_OK;
+}
+
+template <int MODE>
+__device__ __forceinline__ int32_t auth_any(uintptr_t base, uint32_t& pos, uint32_t end, uint64_t rec_off,
+                                            uint64_t slot, onc_auth& a, onc_unix_params* uo) {
+    if (MODE == ONC_DECODE_BYTES) return auth_bytes(base, pos, end, rec_off, slot, a, uo);
+    return auth_slice(base, pos, end, rec_off, slot, a, uo);
+}
+
+// RpcMessage::try_from (rpc_message.rs:243-271 / :277-313), flattened.
+template <int MODE>
+__device__ __forceinline__ int32_t parse_record(uintptr_t base, uint64_t L, uint64_t rec_off, uint64_t i,
+                                                onc_msg& m, uint32_t& aux0, uint32_t& aux1,
+                                                onc_unix_params* uo) {
+    constexpr int32_t kShort = Rules<MODE>::kShort;
+    // expected_message_len (rpc_message.rs:343-367) + exact-length check
+    if (L < 4) return ONC_ERR_INCOMPLETE_HEADER;
+    const uint32_t hdr = bswap(load4(base));
+    if ((hdr & 0x80000000u) == 0) return ONC_ERR_FRAGMENTED;
+    const uint32_t want = (hdr & 0x7FFFFFFFu) + 4u;
+    if (L != want) {
+        aux0 = uint32_t(L);
+        aux1 = want;
+        return ONC_ERR_INCOMPLETE_MESSAGE;
+    }
+    const uint32_t end = want;
+    uint32_t pos = 4;
+    uint32_t v;
+    ONC_RD(m.xid);
+    ONC_RD(v);
+    if (v == ONC_MSG_CALL) {
+        m.msg_type = ONC_MSG_CALL;
+        uint32_t rv;
+        ONC_RD(rv);
+        if (rv != 2u) {                                    // call_body.rs:39-42
+            aux0 = rv;
+            return ONC_ERR_INVALID_RPC_VERSION;
+        }
+        ONC_RD(m.u.call.program);
+        ONC_RD(m.u.call.program_version);
+        ONC_RD(m.u.call.procedure);
+        int32_t st = auth_any<MODE>(base, pos, end, rec_off, 2 * i, m.cred, uo);
+        if (st != ONC_OK) return st;
+        st = auth_any<MODE>(base, pos, end, rec_off, 2 * i + 1, m.verf, uo);
+        if (st != ONC_OK) return st;
+        m.payload_off = rec_off + pos;                     // call_body.rs:53-59 (zero copy)
+        m.payload_len = end - pos;
+        return ONC_OK;                                     // serialised_len == L for every call
+    }
+    if (v != ONC_MSG_REPLY) {
+        aux0 = v;
+        return ONC_ERR_INVALID_MESSAGE_TYPE;               // rpc_message.rs:43
+    }
+    m.msg_type = ONC_MSG_REPLY;
+    ONC_RD(v);
+    if (v == ONC_REPLY_ACCEPTED) {
+        m.reply_stat = ONC_REPLY_ACCEPTED;
+        const int32_t st = auth_any<MODE>(base, pos, end, rec_off, 2 * i + 1, m.verf, uo);
+        if (st != ONC_OK) return st;
+        ONC_RD(v);
+        m.stat = uint8_t(v);
+        switch (v) {                                       // accepted_reply.rs:158-174
+            case ONC_ACCEPT_SUCCESS:
+                m.payload_off = rec_off + pos;
+                m.payload_len = end - pos;
+                pos = end;
+                break;
+            case ONC_ACCEPT_PROG_UNAVAIL:
+            case ONC_ACCEPT_PROC_UNAVAIL:
+            case ONC_ACCEPT_GARBAGE_ARGS:
+            case ONC_ACCEPT_SYSTEM_ERR:
+                break;
+            case ONC_ACCEPT_PROG_MISMATCH:
+                ONC_RD(m.u.mismatch.low);
+                ONC_RD(m.u.mismatch.high);
+                break;
+            default:
+                aux0 = v;
+                return ONC_ERR_INVALID_REPLY_STATUS;
+        }
+    } else if (v == ONC_REPLY_DENIED) {
+        m.reply_stat = ONC_REPLY_DENIED;
+        ONC_RD(v);
+        m.stat = uint8_t(v);
+        if (v == ONC_REJECT_RPC_MISMATCH) {                // rejected_reply.rs:46-57
+            ONC_RD(m.u.mismatch.low);
+            ONC_RD(m.u.mismatch.high);
+        } else if (v == ONC_REJECT_AUTH_ERROR) {
+            ONC_RD(v);
+            if (v > ONC_AUTH_STAT_MAX) {                   // rejected_reply.rs:187
+                aux0 = v;
+                return ONC_ERR_INVALID_AUTH_ERROR;
+            }
+            m.auth_stat = uint8_t(v);
+        } else {
+            aux0 = v;
+            return ONC_ERR_INVALID_REJECTED_REPLY_TYPE;
+        }
+    } else {
+        aux0 = v;
+        return ONC_ERR_INVALID_REPLY_TYPE;                 // reply_body.rs:33
+    }
+    // serialised_len() of a reply == bytes consumed; trailing bytes are
+    // IncompleteMessage{buffer_len, expected} (rpc_message.rs:261-267).
+    if (pos != end) {
+        aux0 = uint32_t(L);
+        aux1 = pos;
+        return ONC_ERR_INCOMPLETE_MESSAGE;
+    }
+    return ONC_OK;
+}
+#undef ONC_RD
+
+template <int MODE>
+__global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
+    const uint64_t i = uint64_t(blockIdx.x) * kTile + threadIdx.x;
+    if (i >= a.n) return;
+    const uint64_t b = a.rec_off[i];
+    const uint64_t e = a.rec_off[i + 1];
+    const uint64_t L = e - b;
+    onc_msg m;
+    // zero every field (value-initialisation of the union member too)
+    uint4* mz = reinterpret_cast<uint4*>(&m);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);
+    uint32_t aux0 = 0, aux1 = 0;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire) + b;
+    const int32_t st = parse_record<MODE>(base, L, b, i, m, aux0, aux1, a.out.unix_params);
+    if (st != ONC_OK) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);
+    }
+    uint4* dst = reinterpret_cast<uint4*>(a.out.msgs + i);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = mz[k];
+    a.out.status[i] = st;
+    a.out.aux0[i] = aux0;
+    a.out.aux1[i] = aux1;
+}
+
+hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s) {
+    const uint64_t tiles = num_tiles(a.n);
+    if (mode == ONC_DECODE_BYTES)
+        hipLaunchKernelGGL(decode_kernel<ONC_DECODE_BYTES>, dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
+    else
+        hipLaunchKernelGGL(decode_kernel<ONC_DECODE_SLICE>, dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace onc

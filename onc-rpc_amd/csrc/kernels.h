@@ -1,0 +1,48 @@
+// kernels.h — host-side launchers of the gfx950 kernels (internal to the
+// shared library; the public surface is include/onc_rpc.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/onc_rpc.h"
+
+namespace onc {
+
+struct EncArgs {
+    uint64_t n;
+    const onc_msg* msgs;
+    const onc_unix_params* unix;
+    const uint8_t* auth_arena;
+    const uint8_t* payload_arena;
+    uint8_t* out;
+    uint64_t out_cap;
+    uint64_t* rec_off;      // n + 1
+    int32_t* status;        // n
+    uint32_t* rec_len;      // n, optional
+    uint64_t* tile_sum;     // tiles
+    const uint64_t* tile_base;  // tiles
+};
+
+struct DecArgs {
+    uint64_t n;
+    const uint8_t* wire;
+    const uint64_t* rec_off;
+    onc_decoded out;
+};
+
+// encode.hip
+hipError_t launch_enc_len(const EncArgs& a, hipStream_t s);
+hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s);
+// scan.hip
+hipError_t launch_scan_tiles(const uint64_t* in, uint64_t* out_excl, uint64_t count, uint64_t base,
+                             uint64_t* total_out, hipStream_t s);
+hipError_t launch_len_tiles(const uint32_t* len, uint64_t n, uint64_t* tile_sum, hipStream_t s);
+hipError_t launch_len_apply(const uint32_t* len, uint64_t n, const uint64_t* tile_base, uint64_t* rec_off,
+                            hipStream_t s);
+// decode.hip
+hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s);
+
+inline uint64_t num_tiles(uint64_t n) { return (n + 255) / 256; }
+
+}  // namespace onc

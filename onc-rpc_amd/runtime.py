@@ -1,0 +1,254 @@
+"""ctypes binding of the gfx950 codec library (libonc_rpc_amd.so, C ABI in
+include/onc_rpc.h) with torch tensors as the device memory.
+
+This is plumbing for tests/bench: all codec work runs in the HIP kernels.
+There is no CPU fallback — loading fails loudly when the library is
+missing, and every call that returns a non-zero rc raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import layout as L
+
+_LIB = None
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libonc_rpc_amd.so")
+
+K_NAMES = ["enc_len_kernel", "scan_tiles_kernel", "enc_emit_kernel", "decode_kernel",
+           "len_tiles_kernel", "len_apply_kernel"]
+K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY = range(6)
+
+# every symbol include/onc_rpc.h declares
+EXPORTED = [
+    "onc_abi_version", "onc_codec_create", "onc_codec_destroy", "onc_codec_set_stream",
+    "onc_codec_sync", "onc_codec_reserve", "onc_codec_last_error", "onc_status_str",
+    "onc_codec_enable_timing", "onc_codec_kernel_stats", "onc_codec_reset_stats",
+    "onc_kernel_name", "onc_encode_lengths", "onc_encode", "onc_decode", "onc_scan_lengths",
+]
+
+
+class OncBatch(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("msgs", C.c_void_p), ("unix_params", C.c_void_p),
+                ("auth_arena", C.c_void_p), ("payload_arena", C.c_void_p)]
+
+
+class OncDecoded(C.Structure):
+    _fields_ = [("msgs", C.c_void_p), ("unix_params", C.c_void_p), ("status", C.c_void_p),
+                ("aux0", C.c_void_p), ("aux1", C.c_void_p)]
+
+
+class CodecError(RuntimeError):
+    pass
+
+
+def load_library(path=LIB_PATH):
+    """Load libonc_rpc_amd.so (raises if it has not been built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise CodecError(f"HIP codec library missing: {path} (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    vp, u64, i32 = C.c_void_p, C.c_uint64, C.c_int
+    lib.onc_abi_version.restype = i32
+    lib.onc_codec_create.argtypes = [C.POINTER(vp), i32, vp]
+    lib.onc_codec_destroy.argtypes = [vp]
+    lib.onc_codec_set_stream.argtypes = [vp, vp]
+    lib.onc_codec_sync.argtypes = [vp]
+    lib.onc_codec_reserve.argtypes = [vp, u64]
+    lib.onc_codec_last_error.argtypes = [vp]
+    lib.onc_codec_last_error.restype = C.c_char_p
+    lib.onc_status_str.argtypes = [C.c_int32]
+    lib.onc_status_str.restype = C.c_char_p
+    lib.onc_codec_enable_timing.argtypes = [vp, i32]
+    lib.onc_codec_kernel_stats.argtypes = [vp, vp, vp]
+    lib.onc_codec_reset_stats.argtypes = [vp]
+    lib.onc_kernel_name.argtypes = [i32]
+    lib.onc_kernel_name.restype = C.c_char_p
+    lib.onc_encode_lengths.argtypes = [vp, C.POINTER(OncBatch), vp, vp]
+    lib.onc_encode.argtypes = [vp, C.POINTER(OncBatch), vp, u64, vp, vp, vp]
+    lib.onc_decode.argtypes = [vp, vp, vp, u64, i32, C.POINTER(OncDecoded)]
+    lib.onc_scan_lengths.argtypes = [vp, vp, u64, u64, vp]
+    for name in EXPORTED:
+        getattr(lib, name).restype = getattr(lib, name).restype or i32
+    _LIB = lib
+    return lib
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def to_device(arr, device):
+    """numpy array -> uint8 CUDA tensor holding its bytes."""
+    torch = _torch()
+    raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+    if raw.size == 0:
+        raw = np.zeros(16, np.uint8)
+    return torch.from_numpy(raw.copy()).to(device)
+
+
+class DeviceBatch:
+    """Descriptor batch resident in HBM (torch uint8 tensors)."""
+
+    def __init__(self, n, msgs, unix, auth_arena, payload_arena):
+        self.n = n
+        self.msgs = msgs
+        self.unix = unix
+        self.auth_arena = auth_arena
+        self.payload_arena = payload_arena
+
+    @classmethod
+    def from_host(cls, hb: L.HostBatch, device="cuda"):
+        return cls(hb.n, to_device(hb.msgs, device), to_device(hb.unix, device),
+                   to_device(hb.auth_arena, device), to_device(hb.payload_arena, device))
+
+    def c_struct(self):
+        return OncBatch(self.n, self.msgs.data_ptr(), self.unix.data_ptr(),
+                        self.auth_arena.data_ptr(), self.payload_arena.data_ptr())
+
+
+class Codec:
+    """One onc_codec handle bound to a device and (by default) torch's
+    current stream on that device."""
+
+    def __init__(self, device=0, stream=None):
+        torch = _torch()
+        self.lib = load_library()
+        self.device = device
+        if stream is None:
+            stream = torch.cuda.current_stream(device).cuda_stream
+        self.stream = stream
+        h = C.c_void_p()
+        rc = self.lib.onc_codec_create(C.byref(h), device, C.c_void_p(stream))
+        if rc != 0:
+            raise CodecError(f"onc_codec_create rc={rc}")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.onc_codec_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            err = self.lib.onc_codec_last_error(self.h).decode()
+            raise CodecError(f"{what} rc={rc} {err}")
+
+    def sync(self):
+        self._check(self.lib.onc_codec_sync(self.h), "onc_codec_sync")
+
+    def reserve(self, n):
+        self._check(self.lib.onc_codec_reserve(self.h, n), "onc_codec_reserve")
+
+    def enable_timing(self, on=True):
+        self._check(self.lib.onc_codec_enable_timing(self.h, 1 if on else 0), "enable_timing")
+
+    def kernel_stats(self):
+        ms = (C.c_double * 6)()
+        cnt = (C.c_uint64 * 6)()
+        self._check(self.lib.onc_codec_kernel_stats(self.h, C.cast(ms, C.c_void_p), C.cast(cnt, C.c_void_p)),
+                    "kernel_stats")
+        return {K_NAMES[k]: (ms[k], cnt[k]) for k in range(6)}
+
+    def reset_stats(self):
+        self._check(self.lib.onc_codec_reset_stats(self.h), "reset_stats")
+
+    # -- encode -----------------------------------------------------------
+    def encode_lengths(self, batch: DeviceBatch, rec_len, status):
+        b = batch.c_struct()
+        self._check(self.lib.onc_encode_lengths(self.h, C.byref(b), _ptr(rec_len), _ptr(status)),
+                    "onc_encode_lengths")
+
+    def encode(self, batch: DeviceBatch, out, rec_off, status, rec_len=None, out_cap=None):
+        b = batch.c_struct()
+        cap = out.numel() if out_cap is None else out_cap
+        self._check(self.lib.onc_encode(self.h, C.byref(b), _ptr(out), cap, _ptr(rec_off), _ptr(status),
+                                        _ptr(rec_len)), "onc_encode")
+
+    # -- decode -----------------------------------------------------------
+    def decode(self, wire, rec_off, n, mode, msgs, unix, status, aux0, aux1):
+        d = OncDecoded(msgs.data_ptr(), unix.data_ptr(), status.data_ptr(), aux0.data_ptr(),
+                       aux1.data_ptr())
+        self._check(self.lib.onc_decode(self.h, _ptr(wire), _ptr(rec_off), n, mode, C.byref(d)),
+                    "onc_decode")
+
+    def scan_lengths(self, rec_len, n, base, rec_off):
+        self._check(self.lib.onc_scan_lengths(self.h, _ptr(rec_len), n, base, _ptr(rec_off)),
+                    "onc_scan_lengths")
+
+
+class DecodeBuffers:
+    """Device output buffers for a decode of n records."""
+
+    def __init__(self, n, device="cuda"):
+        torch = _torch()
+        self.n = n
+        m = max(n, 1)
+        self.msgs = torch.empty(m * 64, dtype=torch.uint8, device=device)
+        self.unix = torch.empty(2 * m * 96, dtype=torch.uint8, device=device)
+        self.status = torch.empty(m, dtype=torch.int32, device=device)
+        self.aux0 = torch.empty(m, dtype=torch.int32, device=device)
+        self.aux1 = torch.empty(m, dtype=torch.int32, device=device)
+
+    def to_host(self):
+        msgs = self.msgs.cpu().numpy().view(L.MSG_DTYPE)[: self.n]
+        unix = self.unix.cpu().numpy().view(L.UNIX_DTYPE)[: 2 * self.n]
+        return (msgs, unix, self.status.cpu().numpy()[: self.n].copy(),
+                self.aux0.cpu().numpy().view(np.uint32)[: self.n].copy(),
+                self.aux1.cpu().numpy().view(np.uint32)[: self.n].copy())
+
+
+def encode_host_batch(codec: Codec, hb: L.HostBatch, device="cuda", out_cap=None):
+    """Convenience: host batch -> GPU encode -> (wire bytes, rec_off, status, rec_len) on host."""
+    torch = _torch()
+    db = DeviceBatch.from_host(hb, device)
+    n = hb.n
+    lens = codec_lengths(codec, db)
+    total = int(lens.sum())
+    cap = total if out_cap is None else out_cap
+    out = torch.zeros(max(16, (cap + 15) // 16 * 16), dtype=torch.uint8, device=device)
+    rec_off = torch.empty(n + 1, dtype=torch.int64, device=device)
+    status = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    rec_len = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    codec.encode(db, out, rec_off, status, rec_len, out_cap=cap)
+    codec.sync()
+    return (out.cpu().numpy()[:min(total, cap)].tobytes(), rec_off.cpu().numpy().view(np.uint64).copy(),
+            status.cpu().numpy()[:n].copy(), rec_len.cpu().numpy().view(np.uint32)[:n].copy())
+
+
+def codec_lengths(codec: Codec, db: DeviceBatch):
+    torch = _torch()
+    n = db.n
+    rec_len = torch.empty(max(n, 1), dtype=torch.int32, device=db.msgs.device)
+    status = torch.empty(max(n, 1), dtype=torch.int32, device=db.msgs.device)
+    if n:
+        codec.encode_lengths(db, rec_len, status)
+        codec.sync()
+    return rec_len.cpu().numpy().view(np.uint32)[:n].astype(np.uint64)
+
+
+def decode_host_wire(codec: Codec, wire: np.ndarray, rec_off: np.ndarray, mode, device="cuda"):
+    """Convenience: packed wire + offsets (host) -> GPU decode -> host arrays."""
+    torch = _torch()
+    n = len(rec_off) - 1
+    w = to_device(wire, device)
+    off = torch.from_numpy(rec_off.astype(np.uint64).view(np.int64).copy()).to(device)
+    bufs = DecodeBuffers(n, device)
+    codec.decode(w, off, n, mode, bufs.msgs, bufs.unix, bufs.status, bufs.aux0, bufs.aux1)
+    codec.sync()
+    return bufs.to_host()

@@ -1,0 +1,314 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the CPU oracle,
+the reference's golden vectors and round-trip invariants.
+
+Bit-exact for everything (integer/byte work): wire bytes, record offsets,
+per-record status + aux, decoded descriptors and AUTH_UNIX slots.
+"""
+import numpy as np
+import pytest
+
+import onc_rpc_amd.layout as L
+import onc_rpc_amd.synth as S
+
+pytestmark = pytest.mark.gpu
+
+MODES = [L.DECODE_SLICE, L.DECODE_BYTES]
+
+
+@pytest.fixture(scope="module")
+def codec():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    import onc_rpc_amd.runtime as R
+    c = R.Codec(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def R():
+    import onc_rpc_amd.runtime as R
+    return R
+
+
+def unix_slots_used(msgs, status):
+    """(slot index, mask) of AUTH_UNIX slots defined for OK records."""
+    ok = status == 0
+    cred = ok & (msgs["msg_type"] == L.MSG_CALL) & ((msgs["cred_kind_len"] >> 24) == L.KIND_UNIX)
+    verf = ok & ((msgs["msg_type"] == L.MSG_CALL) | (msgs["reply_stat"] == L.REPLY_ACCEPTED)) & \
+        ((msgs["verf_kind_len"] >> 24) == L.KIND_UNIX)
+    idx = np.concatenate([2 * np.nonzero(cred)[0], 2 * np.nonzero(verf)[0] + 1])
+    return np.sort(idx)
+
+
+def assert_decoded_equal(gpu, ora, what=""):
+    gm, gu, gs, ga0, ga1 = gpu
+    om, ou, os_, oa0, oa1 = ora
+    bad = np.nonzero(gs != os_)[0]
+    assert len(bad) == 0, f"{what} status mismatch at {bad[:10]}: gpu {gs[bad[:10]]} oracle {os_[bad[:10]]}"
+    bad = np.nonzero((ga0 != oa0) | (ga1 != oa1))[0]
+    assert len(bad) == 0, f"{what} aux mismatch at {bad[:10]}"
+    gb = gm.view(np.uint8).reshape(-1, 64)
+    ob = om.view(np.uint8).reshape(-1, 64)
+    bad = np.nonzero((gb != ob).any(axis=1))[0]
+    assert len(bad) == 0, f"{what} descriptor mismatch at {bad[:10]}: {gm[bad[0]]} vs {om[bad[0]]}"
+    idx = unix_slots_used(om, os_)
+    if len(idx):
+        gbu = gu.view(np.uint8).reshape(-1, 96)[idx]
+        obu = ou.view(np.uint8).reshape(-1, 96)[idx]
+        bad = np.nonzero((gbu != obu).any(axis=1))[0]
+        assert len(bad) == 0, f"{what} unix slot mismatch at {idx[bad[:10]]}"
+
+
+def gpu_vs_oracle_encode(R, codec, oracle, hb, out_cap=None):
+    g_wire, g_off, g_st, g_len = R.encode_host_batch(codec, hb, out_cap=out_cap)
+    o_wire, o_off, o_st, o_len = oracle.encode_batch(hb, out_cap=out_cap)
+    assert np.array_equal(g_st, o_st), f"status {np.nonzero(g_st != o_st)[0][:10]}"
+    assert np.array_equal(g_off, o_off), f"rec_off {np.nonzero(g_off != o_off)[0][:10]}"
+    assert np.array_equal(g_len, o_len)
+    if g_wire != o_wire:
+        a = np.frombuffer(g_wire, np.uint8)
+        b = np.frombuffer(o_wire, np.uint8)
+        n = min(len(a), len(b))
+        first = int(np.nonzero(a[:n] != b[:n])[0][0]) if (a[:n] != b[:n]).any() else n
+        rec = int(np.searchsorted(o_off, first, side="right") - 1)
+        raise AssertionError(f"wire differs first at byte {first} (record {rec}); len {len(a)} vs {len(b)}")
+    return o_wire, o_off, o_st
+
+
+def all_golden_records(golden):
+    recs, names = [], []
+    for sect in ("messages", "errors", "xdrlib", "derived_errors"):
+        for v in golden[sect]:
+            recs.append(bytes.fromhex(v["hex"]))
+            names.append((sect, v))
+    return recs, names
+
+
+# ---------------------------------------------------------------------------
+def test_golden_decode_both_modes(codec, R, oracle, golden):
+    recs, names = all_golden_records(golden)
+    # each record in a batch twice: at an aligned and a misaligned start
+    recs = recs + [r for r in recs]
+    wire, off = L.records_from_wire(recs)
+    for mode in MODES:
+        g = R.decode_host_wire(codec, wire, off, mode)
+        o = oracle.decode_batch(wire, off, mode)
+        assert_decoded_equal(g, o, f"mode {mode}")
+        gm, gu, gs, ga0, ga1 = g
+        mode_name = "bytes" if mode == L.DECODE_BYTES else "slice"
+        for i, (sect, v) in enumerate(names):
+            if sect in ("messages", "xdrlib"):
+                assert gs[i] == 0, v["name"]
+            elif sect == "errors":
+                assert gs[i] == v["expect"]["status"], v["name"]
+                if "aux0" in v["expect"]:
+                    assert (ga0[i], ga1[i]) == (v["expect"]["aux0"], v["expect"]["aux1"])
+            else:
+                e = v["expect_by_mode"][mode_name]
+                assert gs[i] == e["status"], (v["name"], mode_name, gs[i])
+                if "aux0" in e:
+                    assert ga0[i] == e["aux0"]
+            if sect == "xdrlib":
+                assert L.describe(gm[i], gu, wire) == v["expect_full"], v["name"]
+
+
+def test_golden_reencode_from_decoded(codec, R, oracle, golden):
+    """serialise(try_from(buf)) == buf on the GPU for every golden message
+    (rpc_message.rs:578-579, :826-827, :877-878; fuzz parse_serialise)."""
+    recs = [bytes.fromhex(v["hex"]) for s in ("messages", "xdrlib") for v in golden[s]]
+    wire, off = L.records_from_wire(recs)
+    gm, gu, gs, _, _ = R.decode_host_wire(codec, wire, off, L.DECODE_SLICE)
+    assert (gs == 0).all()
+    hb = L.HostBatch(gm.copy(), gu.copy(), wire, wire)
+    g_wire, g_off, g_st, _ = R.encode_host_batch(codec, hb)
+    assert (g_st == 0).all()
+    assert np.array_equal(g_off, off)
+    assert g_wire == b"".join(recs)
+
+
+def test_golden_encode_from_builder(codec, R, oracle, golden):
+    msgs = [v["expect_full"] for v in golden["xdrlib"]]
+    hb = L.build_batch(msgs)
+    wire, off, st = gpu_vs_oracle_encode(R, codec, oracle, hb)
+    assert wire == b"".join(bytes.fromhex(v["hex"]) for v in golden["xdrlib"])
+
+
+@pytest.mark.parametrize("gen", ["call_none", "call_unix16", "cpu_roundtrip", "mixed", "mixed_exotic"])
+def test_encode_configs_bit_exact(codec, R, oracle, gen):
+    hb = {"call_none": lambda: S.call_none(5000, 256),
+          "call_unix16": lambda: S.call_unix16(3000, 1024),
+          "cpu_roundtrip": lambda: S.cpu_roundtrip(2000),
+          "mixed": lambda: S.mixed(4000, seed=5),
+          "mixed_exotic": lambda: S.mixed(4000, seed=6, pmin=0, pmax=300, exotic=0.3)}[gen]()
+    wire, off, st = gpu_vs_oracle_encode(R, codec, oracle, hb)
+    assert (st == 0).all()
+    # and decode the result back on the GPU, both modes, against the oracle
+    w = np.frombuffer(wire + b"\0" * 16, np.uint8).copy()
+    for mode in MODES:
+        g = R.decode_host_wire(codec, w, off, mode)
+        o = oracle.decode_batch(w, off, mode)
+        assert_decoded_equal(g, o, gen)
+        assert (g[2] == 0).all()
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_random_messages_round_trip(codec, R, oracle, seed):
+    """prop_round_trip (rpc_message.rs:1128-1154) over the reference's
+    strategies: serialise == oracle, serialised_len == bytes written,
+    expected_message_len == len, and decode -> describe == original."""
+    ms = S.random_messages(1500, seed=seed)
+    hb = L.build_batch(ms)
+    wire, off, st = gpu_vs_oracle_encode(R, codec, oracle, hb)
+    assert (st == 0).all()
+    w = np.frombuffer(wire + b"\0" * 16, np.uint8).copy()
+    lens = np.diff(off)
+    hdr = w[off[:-1, None].astype(np.int64) + np.arange(4)[None, :]]
+    explen = ((hdr[:, 0].astype(np.uint64) & 0x7F) << 24 | hdr[:, 1].astype(np.uint64) << 16 |
+              hdr[:, 2].astype(np.uint64) << 8 | hdr[:, 3].astype(np.uint64)) + 4
+    assert np.array_equal(explen, lens)
+    for mode in MODES:
+        g = R.decode_host_wire(codec, w, off, mode)
+        assert_decoded_equal(g, oracle.decode_batch(w, off, mode))
+        gm, gu, gs, _, _ = g
+        assert (gs == 0).all()
+        for i in range(len(ms)):
+            want = dict(ms[i])
+            for k in ("cred", "verf"):
+                if k in want and want[k]["kind"] == "none" and not want[k]["data"]:
+                    want[k] = {"kind": "none", "data": None}
+            got = L.describe(gm[i], gu, w)
+            assert got == want, i
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_corrupted_records_first_error(codec, R, oracle, mode):
+    """Fuzz-style mutated records: first-error parity (status + aux)."""
+    hb = L.build_batch(S.random_messages(1200, seed=21, max_payload=64))
+    wire, off, _ = oracle.encode_batch(hb)[:3]
+    w = np.frombuffer(wire + b"\0" * 16, np.uint8).copy()
+    cw, coff = S.corrupt(w, off, frac=0.6, seed=int(mode) + 3)
+    g = R.decode_host_wire(codec, cw, coff, mode)
+    o = oracle.decode_batch(cw, coff, mode)
+    assert_decoded_equal(g, o, "corrupt")
+    assert (o[2] != 0).sum() > 200
+
+
+def test_slice_vs_bytes_fuzz_invariant(codec, R, oracle):
+    """fuzz/fuzz_targets/bytes.rs: slice and Bytes decoders agree on Ok/Err and
+    the successful decodes re-serialise identically."""
+    hb = L.build_batch(S.random_messages(800, seed=31, max_payload=40))
+    wire, off, _ = oracle.encode_batch(hb)[:3]
+    w = np.frombuffer(wire + b"\0" * 16, np.uint8).copy()
+    cw, coff = S.corrupt(w, off, frac=0.7, seed=9)
+    gs = R.decode_host_wire(codec, cw, coff, L.DECODE_SLICE)
+    gb = R.decode_host_wire(codec, cw, coff, L.DECODE_BYTES)
+    assert np.array_equal(gs[2] == 0, gb[2] == 0)
+    ok = np.nonzero(gs[2] == 0)[0]
+    a = R.encode_host_batch(codec, L.HostBatch(gs[0][ok].copy(), gs[1], cw, cw))[0]
+    b = R.encode_host_batch(codec, L.HostBatch(gb[0][ok].copy(), gb[1], cw, cw))[0]
+    assert a == b
+
+
+def test_encode_panic_statuses(codec, R, oracle):
+    none = {"kind": "none", "data": None}
+
+    def call(cred, verf=none):
+        return {"xid": 1, "type": "call", "program": 1, "program_version": 1, "procedure": 1,
+                "cred": cred, "verf": verf, "payload": "ab"}
+
+    def unix(nl, ng):
+        return {"kind": "unix", "stamp": 42, "machine_name": "01" * nl, "uid": 42, "gid": 42, "gids": list(range(ng))}
+
+    ms = [call(unix(255, 0)), call(unix(256, 0)), call(unix(0, 16)), call(unix(124, 16)),
+          call(unix(125, 16)), call({"kind": "short", "data": "00" * 201}),
+          call(none, {"kind": "unknown", "id": 7, "data": "11" * 201}), call(none)]
+    hb = L.build_batch(ms)
+    hb.unix["ngids"][2] = 17          # Gids::from_iter panic (> 16), unix_params.rs:47
+    hb.msgs["msg_type"][7] = 5        # unrepresentable descriptor
+    wire, off, st = gpu_vs_oracle_encode(R, codec, oracle, hb)
+    assert list(st) == [101, 102, 103, 0, 101, 101, 101, 104]
+
+
+def test_write_zero_capacity(codec, R, oracle):
+    hb = S.mixed(700, seed=8, pmin=0, pmax=200)
+    total = int(oracle.encode_batch(hb)[1][-1])
+    for cap in (0, 37, total // 3, total - 1, total):
+        gpu_vs_oracle_encode(R, codec, oracle, hb, out_cap=cap)
+
+
+def test_unaligned_arenas(codec, R, oracle):
+    """Payload/auth bodies at every byte alignment in the arenas."""
+    base = L.build_batch(S.random_messages(600, seed=41, max_payload=70))
+    for shift in (1, 2, 3):
+        pay = np.concatenate([np.zeros(shift, np.uint8), base.payload_arena])
+        auth = np.concatenate([np.zeros(4 - shift, np.uint8), base.auth_arena])
+        msgs = base.msgs.copy()
+        unix = base.unix.copy()
+        msgs["payload_off"] += shift
+        for f in ("cred", "verf"):
+            opaque = (msgs[f + "_kind_len"] >> 24) != L.KIND_UNIX
+            msgs[f + "_ref"][opaque] += 4 - shift
+        unix["name_off"] += 4 - shift
+        gpu_vs_oracle_encode(R, codec, oracle, L.HostBatch(msgs, unix, auth, pay))
+
+
+def test_empty_and_single(codec, R, oracle):
+    import torch
+    hb = S.call_none(1, 0)
+    gpu_vs_oracle_encode(R, codec, oracle, hb)
+    db = R.DeviceBatch(0, *(torch.zeros(16, dtype=torch.uint8, device="cuda") for _ in range(4)))
+    out = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    rec_off = torch.full((1,), 7, dtype=torch.int64, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    codec.encode(db, out, rec_off, st)
+    codec.sync()
+    assert int(rec_off[0]) == 0
+    # decode of zero records is a no-op
+    bufs = R.DecodeBuffers(0)
+    codec.decode(out, rec_off, 0, 0, bufs.msgs, bufs.unix, bufs.status, bufs.aux0, bufs.aux1)
+    codec.sync()
+
+
+def test_scan_lengths(codec, R):
+    import torch
+    rng = np.random.default_rng(3)
+    for n in (1, 255, 256, 257, 100000):
+        lens = rng.integers(0, 5000, n).astype(np.uint32)
+        d = torch.from_numpy(lens.view(np.int32).copy()).cuda()
+        off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        codec.scan_lengths(d, n, 12345, off)
+        codec.sync()
+        want = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))]) + 12345
+        assert np.array_equal(off.cpu().numpy().view(np.uint64), want)
+
+
+def test_full_size_config1_loopback(codec, R, oracle):
+    """configs[1] at full size (1M x 256 B): encode -> decode on the GPU with
+    size-independent checks (all OK, xids, offsets, payload bytes, lengths),
+    plus a bit-exact oracle comparison of a 20k-record window."""
+    import torch
+    n = 1_000_000
+    hb = S.call_none(n, 256)
+    db = R.DeviceBatch.from_host(hb)
+    out = torch.empty(n * 300 + 16, dtype=torch.uint8, device="cuda")
+    rec_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    codec.encode(db, out, rec_off, st)
+    bufs = R.DecodeBuffers(n)
+    codec.decode(out, rec_off, n, L.DECODE_SLICE, bufs.msgs, bufs.unix, bufs.status, bufs.aux0, bufs.aux1)
+    codec.sync()
+    assert int((st != 0).sum()) == 0
+    assert torch.equal(rec_off, torch.arange(n + 1, device="cuda", dtype=torch.int64) * 300)
+    assert int((bufs.status != 0).sum()) == 0
+    dm = bufs.msgs.view(-1, 64)
+    xid = dm[:, 0:4].contiguous().view(torch.int32).view(-1)
+    assert torch.equal(xid, torch.arange(n, device="cuda", dtype=torch.int32))
+    # payload bytes of every record == payload arena (gather by offsets)
+    wire_payload = out[: n * 300].view(n, 300)[:, 44:]
+    assert torch.equal(wire_payload.reshape(-1), db.payload_arena[: n * 256])
+    # bit-exact window vs the oracle
+    lo, hi = 500_000, 520_000
+    sub = L.HostBatch(hb.msgs[lo:hi].copy(), hb.unix, hb.auth_arena, hb.payload_arena)
+    o_wire = oracle.encode_batch(sub)[0]
+    assert out[lo * 300:hi * 300].cpu().numpy().tobytes() == o_wire
