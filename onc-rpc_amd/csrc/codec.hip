@@ -146,7 +146,7 @@ int onc_codec_sync(onc_codec* c) {
 int onc_codec_reserve(onc_codec* c, uint64_t max_records) {
     if (!c) return ONC_RC_EINVAL;
     if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
-    return ensure_scratch(c, onc::num_tiles(max_records));
+    return ensure_scratch(c, onc::num_emit_tiles(max_records));
 }
 
 const char* onc_codec_last_error(const onc_codec* c) { return c ? c->last_error.c_str() : "null codec"; }
@@ -239,7 +239,7 @@ int onc_encode_lengths(onc_codec* c, const onc_batch* batch, uint32_t* rec_len, 
     if (!c || check_batch(batch) != ONC_RC_OK || (batch->n && (!rec_len || !status))) return ONC_RC_EINVAL;
     if (batch->n == 0) return ONC_RC_OK;
     if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
-    const uint64_t tiles = onc::num_tiles(batch->n);
+    const uint64_t tiles = onc::num_emit_tiles(batch->n);
     int rc = ensure_scratch(c, tiles);
     if (rc != ONC_RC_OK) return rc;
     onc::EncArgs a{};
@@ -264,7 +264,7 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
         const hipError_t e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
         return e == hipSuccess ? ONC_RC_OK : fail(c, e, "hipMemsetAsync");
     }
-    const uint64_t tiles = onc::num_tiles(batch->n);
+    const uint64_t tiles = onc::num_emit_tiles(batch->n);
     int rc = ensure_scratch(c, tiles);
     if (rc != ONC_RC_OK) return rc;
     onc::EncArgs a{};

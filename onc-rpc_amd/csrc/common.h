@@ -15,6 +15,7 @@ namespace onc {
 
 constexpr int kTile = 256;        // records per tile (= threads per block)
 constexpr int kScanThreads = 1024;
+constexpr int kEmitRecs = 128;   // records per encode tile (enc_len totals, enc_emit workgroup)
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -28,17 +29,27 @@ __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh
 __host__ __device__ __forceinline__ uint32_t pad4(uint32_t l) { return (4u - (l & 3u)) & 3u; }
 __host__ __device__ __forceinline__ uint32_t words4(uint32_t l) { return (l + 3u) >> 2; }
 
+// Loads through address_space(1) pointers: plain integer addresses would
+// otherwise lower to flat_load (which also waits on lgkmcnt).
+#define ONC_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ T gload(uintptr_t a) {
+    return *(const ONC_GLOBAL T*)a;
+}
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 // Four stream bytes at absolute byte address `addr`, bytes at or beyond
 // `lim` read as zero. Precondition: addr < lim. Only aligned dwords that
 // contain at least one byte < lim are touched, so the read never leaves
-// the valid range's pages.
+// the valid range's pages. Branch-free (both loads always issue).
 __device__ __forceinline__ uint32_t load4_masked(uintptr_t addr, uintptr_t lim) {
     const uintptr_t al = addr & ~uintptr_t(3);
     const uint32_t sh = uint32_t(addr & 3);
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(al);
-    const uint32_t w0 = p[0];
-    const uint32_t w1 = (sh != 0 && al + 4 < lim) ? p[1] : 0u;
-    uint32_t v = funnel(w0, w1, sh);
+    const bool second = sh != 0 && al + 4 < lim;
+    const uint32_t w0 = gload<uint32_t>(al);
+    const uint32_t w1 = gload<uint32_t>(al + (second ? 4 : 0));
+    uint32_t v = funnel(w0, second ? w1 : 0u, sh);
     const uintptr_t n = lim - addr;
     if (n < 4) v &= (1u << (8u * uint32_t(n))) - 1u;
     return v;
@@ -48,10 +59,22 @@ __device__ __forceinline__ uint32_t load4_masked(uintptr_t addr, uintptr_t lim) 
 __device__ __forceinline__ uint32_t load4(uintptr_t addr) {
     const uintptr_t al = addr & ~uintptr_t(3);
     const uint32_t sh = uint32_t(addr & 3);
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(al);
-    const uint32_t w0 = p[0];
-    const uint32_t w1 = sh ? p[1] : 0u;
-    return funnel(w0, w1, sh);
+    const uint32_t w0 = gload<uint32_t>(al);
+    const uint32_t w1 = gload<uint32_t>(al + (sh ? 4 : 0));
+    return funnel(w0, sh ? w1 : 0u, sh);
+}
+
+// 16 bytes at an arbitrary byte address, all valid: one dwordx4 load at the
+// 4-aligned address below it, one more dword, v_alignbyte.
+__device__ __forceinline__ void load16_unaligned(uintptr_t addr, uint32_t v[4]) {
+    const uintptr_t al = addr & ~uintptr_t(3);
+    const uint32_t sh = uint32_t(addr & 3);
+    const u32x4_a4 w = gload<u32x4_a4>(al);
+    const uint32_t w4 = gload<uint32_t>(al + (sh ? 16 : 12));
+    v[0] = funnel(w.x, w.y, sh);
+    v[1] = funnel(w.y, w.z, sh);
+    v[2] = funnel(w.z, w.w, sh);
+    v[3] = funnel(w.w, sh ? w4 : 0u, sh);
 }
 
 // ---------------------------------------------------------------------------
@@ -235,6 +258,66 @@ __device__ __forceinline__ uint32_t record_word(const onc_msg& d, uint32_t len, 
     const uint64_t j = uint64_t(k) - hw;
     const uintptr_t b = s.payload_arena + d.payload_off;
     return load4_masked(b + 4 * j, b + d.payload_len);
+}
+
+// Sequential serialiser of the header words of one planned record (the
+// serialise_into call chain in write order), used to stage headers in LDS.
+// Writes meta_hw(meta) words to dst[0..hw).
+__device__ __forceinline__ uint32_t put_auth_words(const onc_auth& a, const EncSrc& s, uint32_t* dst, uint32_t k) {
+    const uint32_t kind = a.kind_len >> 24;
+    dst[k++] = bswap(kind == ONC_KIND_UNKNOWN ? a.id : kind);
+    if (kind != ONC_KIND_UNIX) {
+        const uint32_t len = a.kind_len & 0xFFFFFFu;
+        dst[k++] = bswap(len);
+        const uintptr_t b = s.auth_arena + a.ref;
+        for (uint32_t j = 0; 4 * j < len; ++j) dst[k++] = load4_masked(b + 4ull * j, b + len);
+        return k;
+    }
+    const onc_unix_params* u = s.unix + a.ref;
+    const uint32_t nl = u->name_len, ng = u->ngids;
+    dst[k++] = bswap(20u + 4u * words4(nl) + 4u * ng);
+    dst[k++] = bswap(u->stamp);
+    dst[k++] = bswap(nl);
+    const uintptr_t b = s.auth_arena + u->name_off;
+    for (uint32_t j = 0; 4 * j < nl; ++j) dst[k++] = load4_masked(b + 4ull * j, b + nl);
+    dst[k++] = bswap(u->uid);
+    dst[k++] = bswap(u->gid);
+    dst[k++] = bswap(ng);
+    for (uint32_t j = 0; j < ng; ++j) dst[k++] = bswap(u->gids[j]);
+    return k;
+}
+
+__device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, uint32_t* dst) {
+    uint32_t k = 0;
+    dst[k++] = bswap((len - 4u) | 0x80000000u);
+    dst[k++] = bswap(d.xid);
+    dst[k++] = bswap(uint32_t(d.msg_type));
+    if (d.msg_type == ONC_MSG_CALL) {
+        dst[k++] = bswap(2u);
+        dst[k++] = bswap(d.u.call.program);
+        dst[k++] = bswap(d.u.call.program_version);
+        dst[k++] = bswap(d.u.call.procedure);
+        k = put_auth_words(d.cred, s, dst, k);
+        put_auth_words(d.verf, s, dst, k);
+        return;
+    }
+    dst[k++] = bswap(uint32_t(d.reply_stat));
+    if (d.reply_stat == ONC_REPLY_ACCEPTED) {
+        k = put_auth_words(d.verf, s, dst, k);
+        dst[k++] = bswap(uint32_t(d.stat));
+        if (d.stat == ONC_ACCEPT_PROG_MISMATCH) {
+            dst[k++] = bswap(d.u.mismatch.low);
+            dst[k++] = bswap(d.u.mismatch.high);
+        }
+        return;
+    }
+    dst[k++] = bswap(uint32_t(d.stat));
+    if (d.stat == ONC_REJECT_RPC_MISMATCH) {
+        dst[k++] = bswap(d.u.mismatch.low);
+        dst[k++] = bswap(d.u.mismatch.high);
+    } else {
+        dst[k++] = bswap(uint32_t(d.auth_stat));
+    }
 }
 
 // ---------------------------------------------------------------------------

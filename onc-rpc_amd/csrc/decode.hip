@@ -19,11 +19,35 @@
 
 namespace onc {
 
-// Big-endian u32 at record-relative position pos (all 4 bytes valid).
+// Each lane first pulls the first kWinBytes of its record's 16-byte-aligned
+// window into LDS (6 x dwordx4, all issued back to back: one memory latency
+// instead of one per field), laid out [word][lane] so that lanes parsing the
+// same field hit distinct banks. Reads past the window fall back to global.
+constexpr uint32_t kWinWords = 24;
+constexpr uint32_t kWinBytes = 4 * kWinWords;
+
+struct Rd {
+    uintptr_t base;          // absolute address of record byte 0
+    uint32_t q0;             // window offset of record byte 0 (0..15)
+    const uint32_t* col;     // this lane's window column (stride kTile words)
+
+    // Big-endian u32 at record-relative position pos (all 4 bytes valid).
+    __device__ __forceinline__ uint32_t be32(uint32_t pos) const {
+        const uint32_t q = q0 + pos;
+        if (q + 4u <= kWinBytes) {
+            const uint32_t wi = q >> 2, sh = q & 3u;
+            const uint32_t w0 = col[wi * kTile];
+            const uint32_t w1 = sh ? col[(wi + 1) * kTile] : 0u;
+            return bswap(funnel(w0, w1, sh));
+        }
+        return bswap(load4(base + pos));
+    }
+};
+
 #define ONC_RD(var)                                   \
     do {                                              \
         if (pos + 4u > end) return kShort;            \
-        var = bswap(load4(base + pos));               \
+        var = R.be32(pos);                            \
         pos += 4u;                                    \
     } while (0)
 
@@ -37,7 +61,7 @@ struct Rules {
 // Slice mode AuthFlavor::from_cursor (flavor.rs:52-94) with
 // AuthUnixParams::from_cursor (unix_params.rs:90-129) and
 // Opaque::from_wire (opaque.rs:72-98; bound = the whole message, `end`).
-__device__ __forceinline__ int32_t auth_slice(uintptr_t base, uint32_t& pos, uint32_t end, uint64_t rec_off,
+__device__ __forceinline__ int32_t auth_slice(const Rd& R, uint32_t& pos, uint32_t end, uint64_t rec_off,
                                               uint64_t slot, onc_auth& a, onc_unix_params* uo) {
     constexpr int32_t kShort = Rules<ONC_DECODE_SLICE>::kShort;
     uint32_t fl;
@@ -91,7 +115,7 @@ __device__ __forceinline__ int32_t auth_slice(uintptr_t base, uint32_t& pos, uin
 // Bytes mode AuthFlavor::try_from(Bytes) (flavor.rs:190-222): the body is
 // first cut with try_array(200) (bytes_ext.rs:25-42); AUTH_UNIX is parsed
 // inside that slice (unix_params.rs:252-276) and must fill it exactly.
-__device__ __forceinline__ int32_t auth_bytes(uintptr_t base, uint32_t& pos, uint32_t end, uint64_t rec_off,
+__device__ __forceinline__ int32_t auth_bytes(const Rd& R, uint32_t& pos, uint32_t end, uint64_t rec_off,
                                               uint64_t slot, onc_auth& a, onc_unix_params* uo) {
     constexpr int32_t kShort = Rules<ONC_DECODE_BYTES>::kShort;
     uint32_t fl, n;
@@ -109,7 +133,7 @@ __device__ __forceinline__ int32_t auth_bytes(uintptr_t base, uint32_t& pos, uin
 #define ONC_RDQ(var)                                           \
     do {                                                       \
         if (q + 4u > bend) return ONC_ERR_INVALID_LENGTH;      \
-        var = bswap(load4(base + q));                          \
+        var = R.be32(q);                                       \
         q += 4u;                                               \
     } while (0)
         ONC_RDQ(stamp);
@@ -148,21 +172,21 @@ __device__ __forceinline__ int32_t auth_bytes(uintptr_t base, uint32_t& pos, uin
 }
 
 template <int MODE>
-__device__ __forceinline__ int32_t auth_any(uintptr_t base, uint32_t& pos, uint32_t end, uint64_t rec_off,
+__device__ __forceinline__ int32_t auth_any(const Rd& R, uint32_t& pos, uint32_t end, uint64_t rec_off,
                                             uint64_t slot, onc_auth& a, onc_unix_params* uo) {
-    if (MODE == ONC_DECODE_BYTES) return auth_bytes(base, pos, end, rec_off, slot, a, uo);
-    return auth_slice(base, pos, end, rec_off, slot, a, uo);
+    if (MODE == ONC_DECODE_BYTES) return auth_bytes(R, pos, end, rec_off, slot, a, uo);
+    return auth_slice(R, pos, end, rec_off, slot, a, uo);
 }
 
 // RpcMessage::try_from (rpc_message.rs:243-271 / :277-313), flattened.
 template <int MODE>
-__device__ __forceinline__ int32_t parse_record(uintptr_t base, uint64_t L, uint64_t rec_off, uint64_t i,
+__device__ __forceinline__ int32_t parse_record(const Rd& R, uint64_t L, uint64_t rec_off, uint64_t i,
                                                 onc_msg& m, uint32_t& aux0, uint32_t& aux1,
                                                 onc_unix_params* uo) {
     constexpr int32_t kShort = Rules<MODE>::kShort;
     // expected_message_len (rpc_message.rs:343-367) + exact-length check
     if (L < 4) return ONC_ERR_INCOMPLETE_HEADER;
-    const uint32_t hdr = bswap(load4(base));
+    const uint32_t hdr = R.be32(0);
     if ((hdr & 0x80000000u) == 0) return ONC_ERR_FRAGMENTED;
     const uint32_t want = (hdr & 0x7FFFFFFFu) + 4u;
     if (L != want) {
@@ -186,9 +210,9 @@ __device__ __forceinline__ int32_t parse_record(uintptr_t base, uint64_t L, uint
         ONC_RD(m.u.call.program);
         ONC_RD(m.u.call.program_version);
         ONC_RD(m.u.call.procedure);
-        int32_t st = auth_any<MODE>(base, pos, end, rec_off, 2 * i, m.cred, uo);
+        int32_t st = auth_any<MODE>(R, pos, end, rec_off, 2 * i, m.cred, uo);
         if (st != ONC_OK) return st;
-        st = auth_any<MODE>(base, pos, end, rec_off, 2 * i + 1, m.verf, uo);
+        st = auth_any<MODE>(R, pos, end, rec_off, 2 * i + 1, m.verf, uo);
         if (st != ONC_OK) return st;
         m.payload_off = rec_off + pos;                     // call_body.rs:53-59 (zero copy)
         m.payload_len = end - pos;
@@ -202,7 +226,7 @@ __device__ __forceinline__ int32_t parse_record(uintptr_t base, uint64_t L, uint
     ONC_RD(v);
     if (v == ONC_REPLY_ACCEPTED) {
         m.reply_stat = ONC_REPLY_ACCEPTED;
-        const int32_t st = auth_any<MODE>(base, pos, end, rec_off, 2 * i + 1, m.verf, uo);
+        const int32_t st = auth_any<MODE>(R, pos, end, rec_off, 2 * i + 1, m.verf, uo);
         if (st != ONC_OK) return st;
         ONC_RD(v);
         m.stat = uint8_t(v);
@@ -260,19 +284,39 @@ __device__ __forceinline__ int32_t parse_record(uintptr_t base, uint64_t L, uint
 
 template <int MODE>
 __global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
-    const uint64_t i = uint64_t(blockIdx.x) * kTile + threadIdx.x;
+    __shared__ uint32_t s_win[kWinWords * kTile];
+    const int t = threadIdx.x;
+    const uint64_t i = uint64_t(blockIdx.x) * kTile + t;
     if (i >= a.n) return;
     const uint64_t b = a.rec_off[i];
     const uint64_t e = a.rec_off[i + 1];
     const uint64_t L = e - b;
+    const uintptr_t wire = reinterpret_cast<uintptr_t>(a.wire);
+    const uintptr_t base = wire + b;
+    const uintptr_t win = base & ~uintptr_t(15);
+    // Stage the window: all six 16-byte loads issue back to back; chunks
+    // past the record's last byte re-read its last chunk (never leave the
+    // record's 16-byte-aligned span). Empty records read nothing.
+    if (L != 0) {
+        const uintptr_t last = (wire + e - 1) & ~uintptr_t(15);
+        u32x4 v[kWinWords / 4];
+#pragma unroll
+        for (uint32_t j = 0; j < kWinWords / 4; ++j) v[j] = gload<u32x4>(min(win + 16 * j, last));
+#pragma unroll
+        for (uint32_t j = 0; j < kWinWords / 4; ++j) {
+            s_win[(4 * j + 0) * kTile + t] = v[j].x;
+            s_win[(4 * j + 1) * kTile + t] = v[j].y;
+            s_win[(4 * j + 2) * kTile + t] = v[j].z;
+            s_win[(4 * j + 3) * kTile + t] = v[j].w;
+        }
+    }
+    const Rd R{base, uint32_t(base - win), &s_win[t]};
     onc_msg m;
-    // zero every field (value-initialisation of the union member too)
     uint4* mz = reinterpret_cast<uint4*>(&m);
 #pragma unroll
     for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);
     uint32_t aux0 = 0, aux1 = 0;
-    const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire) + b;
-    const int32_t st = parse_record<MODE>(base, L, b, i, m, aux0, aux1, a.out.unix_params);
+    const int32_t st = parse_record<MODE>(R, L, b, i, m, aux0, aux1, a.out.unix_params);
     if (st != ONC_OK) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);

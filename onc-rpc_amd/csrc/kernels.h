@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "../../include/onc_rpc.h"
+#include "common.h"
 
 namespace onc {
 
@@ -44,5 +45,6 @@ hipError_t launch_len_apply(const uint32_t* len, uint64_t n, const uint64_t* til
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s);
 
 inline uint64_t num_tiles(uint64_t n) { return (n + 255) / 256; }
+inline uint64_t num_emit_tiles(uint64_t n) { return (n + kEmitRecs - 1) / kEmitRecs; }
 
 }  // namespace onc
