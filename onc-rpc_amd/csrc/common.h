@@ -15,7 +15,7 @@ namespace onc {
 
 constexpr int kTile = 256;        // records per tile (= threads per block)
 constexpr int kScanThreads = 1024;
-constexpr int kEmitRecs = 128;   // records per encode tile (enc_len totals, enc_emit workgroup)
+constexpr int kEmitRecs = 64;    // records per encode tile = one wavefront (enc_len totals, enc_emit)
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 

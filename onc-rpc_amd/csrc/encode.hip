@@ -27,11 +27,9 @@
 
 namespace onc {
 
-// Per-record plan + per-tile (kEmitRecs records) byte totals. One 256-thread
-// block covers kTile records = 2 emit tiles; tile totals come from the four
-// wave sums.
+// Per-record plan + per-tile (kEmitRecs = 64 records = one wavefront)
+// byte totals: the wave's inclusive __shfl scan, lane 63 writes the total.
 __global__ __launch_bounds__(kTile) void enc_len_kernel(EncArgs a) {
-    __shared__ uint64_t s_wave[kTile / 64];
     const uint64_t r = uint64_t(blockIdx.x) * kTile + threadIdx.x;
     uint64_t len = 0;
     if (r < a.n) {
@@ -42,17 +40,8 @@ __global__ __launch_bounds__(kTile) void enc_len_kernel(EncArgs a) {
         if (a.rec_len) a.rec_len[r] = uint32_t(len);
     }
     const uint64_t incl = wave_incl_scan_u64(len);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 63) s_wave[wave] = incl;
-    __syncthreads();
-    if (threadIdx.x < kTile / kEmitRecs) {
-        constexpr int wpt = kEmitRecs / 64;   // waves per emit tile
-        uint64_t t = 0;
-#pragma unroll
-        for (int w = 0; w < wpt; ++w) t += s_wave[threadIdx.x * wpt + w];
-        const uint64_t tile = uint64_t(blockIdx.x) * (kTile / kEmitRecs) + threadIdx.x;
-        if (tile * kEmitRecs < a.n) a.tile_sum[tile] = t;
-    }
+    const uint64_t tile = r / kEmitRecs;
+    if ((threadIdx.x & 63) == 63 && tile * kEmitRecs < a.n) a.tile_sum[tile] = incl;
 }
 
 // Largest r in [0, nrec) with start[r] <= x (start ascending). Records of
@@ -75,55 +64,68 @@ __device__ __noinline__ uint32_t header_word_slow(const onc_msg* d, uint32_t len
     return header_word(*d, len, meta, k, *src);
 }
 
-constexpr int kHdrCap = 4096;                 // header words staged per tile (16 KiB of LDS)
-constexpr int kMapCap = 4096;                 // 64-byte output granules mapped per tile (256 KiB)
-constexpr uint32_t kNotStaged = 0xFFFFFFFFu;
+constexpr int kHdrCap = 768;                  // header words staged per wave tile (3 KiB)
+constexpr int kMapCap = 512;                  // 64-byte output granules mapped per wave tile (32 KiB)
+constexpr uint16_t kNone16 = 0xFFFFu;
 
-struct EmitTile {
-    uint64_t start[kEmitRecs + 1];   // output offset of each record (+ tile end)
-    uint64_t poff[kEmitRecs];        // payload arena offset
+// Per-record LDS entry, read with two ds_read_b128.
+struct RecEnt {
+    uint64_t start;     // first output byte
+    uint64_t pst;       // first payload byte (start + 4 * header words)
+    uint64_t en;        // one past the last byte
+    uint64_t srcbase;   // payload byte at output offset o lives at srcbase + o
+};
+
+// One wavefront's tile: kEmitRecs records, no workgroup barriers anywhere.
+struct WaveTile {
+    RecEnt ent[kEmitRecs + 1];       // [nrec] = sentinel {T1, T1, T1, 0}
     uint32_t meta[kEmitRecs];        // plan_record() meta (header words etc.)
-    uint32_t hoff[kEmitRecs];        // staged header: word offset in hdr[], or kNotStaged
+    uint16_t hoff[kEmitRecs];        // staged header: word offset in hdr[], or kNone16
     uint32_t hdr[kHdrCap];           // header words of the tile's records (stream order)
     uint8_t map[kMapCap];            // granule g -> record holding byte 64*(G0+g) (or record 0)
 };
 
-// Record holding output byte x (T0 <= x < T1): granule map + short walk
-// over the records that start inside the granule; binary search beyond the
-// mapped range.
-__device__ __forceinline__ int locate(const EmitTile& T, int nrec, uint64_t G0, uint64_t x) {
-    const uint64_t g = (x >> 6) - G0;
-    if (g >= uint64_t(kMapCap)) return find_rec(T.start, nrec, x);
-    int r = T.map[g];
-    while (r + 1 < nrec && T.start[r + 1] <= x) ++r;
-    return r;
+// LDS writes of one lane become visible to the other lanes of the wave.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ uint32_t hdr_word(const EmitTile& T, const EncArgs& a, const EncSrc& src, uint64_t r0,
-                                             int r, uint32_t len, uint32_t meta, uint32_t k) {
-    const uint32_t ho = T.hoff[r];
-    if (ho != kNotStaged) return T.hdr[ho + k];
-    return header_word_slow(a.msgs + r0 + r, len, meta, k, &src);
+__device__ __forceinline__ int find_ent(const RecEnt* ent, int nrec, uint64_t x) {
+    int lo = 0, hi = nrec - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (ent[mid].start <= x) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint32_t hdr_word(const WaveTile& T, const EncArgs& a, const EncSrc& src, uint64_t r0,
+                                             int r, uint32_t len, uint32_t k) {
+    const uint16_t ho = T.hoff[r];
+    if (ho != kNone16) return T.hdr[ho + k];
+    return header_word_slow(a.msgs + r0 + r, len, T.meta[r], k, &src);
 }
 
 // Stream word k of tile record r; 0 outside [0, len).
-__device__ __forceinline__ uint32_t tile_word(const EmitTile& T, const EncArgs& a, const EncSrc& src,
+__device__ __forceinline__ uint32_t tile_word(const WaveTile& T, const EncArgs& a, const EncSrc& src,
                                               uint64_t r0, int r, int64_t k) {
-    const uint64_t st = T.start[r];
-    const uint32_t len = uint32_t(T.start[r + 1] - st);
+    const RecEnt& e = T.ent[r];
+    const uint32_t len = uint32_t(e.en - e.start);
     if (k < 0 || 4 * k >= int64_t(len)) return 0u;
-    const uint32_t meta = T.meta[r];
-    const uint32_t hw = meta_hw(meta);
-    if (uint64_t(k) < hw) return hdr_word(T, a, src, r0, r, len, meta, uint32_t(k));
-    const uintptr_t b = src.payload_arena + T.poff[r];
-    return load4_masked(b + 4 * (uint64_t(k) - hw), b + (len - 4 * hw));
+    const uint32_t hw = uint32_t((e.pst - e.start) >> 2);
+    if (uint64_t(k) < hw) return hdr_word(T, a, src, r0, r, len, uint32_t(k));
+    return load4_masked(e.srcbase + e.start + 4 * uint64_t(k), e.srcbase + e.en);
 }
 
-// Byte-granular chunk: the 16 stream bytes of tile record r at output
-// offsets [o, o+16) (bytes outside the record read as 0).
-__device__ __forceinline__ void tile_chunk(const EmitTile& T, const EncArgs& a, const EncSrc& src, uint64_t r0,
+// Byte-granular: the 16 stream bytes of tile record r at output offsets
+// [o, o+16) (bytes outside the record read as 0).
+__device__ __forceinline__ void tile_chunk(const WaveTile& T, const EncArgs& a, const EncSrc& src, uint64_t r0,
                                            int r, uint64_t o, uint32_t out[4]) {
-    const int64_t rel = int64_t(o) - int64_t(T.start[r]);
+    const int64_t rel = int64_t(o) - int64_t(T.ent[r].start);
     const int64_t k0 = rel >> 2;                 // floor division
     const uint32_t sh = uint32_t(rel & 3);
     uint32_t w[5];
@@ -133,135 +135,196 @@ __device__ __forceinline__ void tile_chunk(const EmitTile& T, const EncArgs& a, 
     for (int i = 0; i < 4; ++i) out[i] = funnel(w[i], w[i + 1], sh);
 }
 
-// Word-aligned chunk (every record of the tile starts and ends on a 4-byte
-// boundary, payload sources 4-aligned): each output dword is one whole
-// stream word of exactly one record.
-__device__ __forceinline__ void aligned_chunk(const EmitTile& T, const EncArgs& a, const EncSrc& src, uint64_t r0,
-                                              int nrec, int r, uint64_t o, uint32_t v[4]) {
-    uint64_t st = T.start[r], en = T.start[r + 1];
+// Next record after r with bytes (skips zero-length records); nrec if none.
+__device__ __forceinline__ int next_rec(const WaveTile& T, int nrec, int r) {
+    ++r;
+    while (r < nrec && T.ent[r].en == T.ent[r].start) ++r;
+    return r;
+}
+
+// Byte-granular special chunk owned by r (tiles holding a record that does
+// not start or end on a 4-byte boundary: unpadded odd-length payloads).
+// Out of line: large, and rare in XDR traffic.
+__device__ __noinline__ void byte_chunk(const WaveTile* Tp, const EncArgs* ap, const EncSrc* srcp, uint64_t r0,
+                                        int nrec, int r, uint64_t o, uint32_t* v) {
+    const WaveTile& T = *Tp;
+    uint32_t w[4];
+    tile_chunk(T, *ap, *srcp, r0, r, o, w);
+    if (o + 16 > T.ent[r].en) {
+        const int r2 = next_rec(T, nrec, r);
+        if (r2 < nrec) {
+            // bytes outside a record read as 0, so the parts OR together
+            uint32_t b[4];
+            tile_chunk(T, *ap, *srcp, r0, r2, o, b);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w[i] |= b[i];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = w[i];
+}
+
+// Word-aligned special chunk owned by r (every record of the tile starts
+// and ends on a 4-byte boundary and reads a 4-aligned payload): each output
+// dword is one whole stream word of r or of the next record.
+__device__ __forceinline__ void aligned_special(const WaveTile& T, const EncArgs& a, const EncSrc& src, uint64_t r0,
+                                                int nrec, int r, const RecEnt& e, uint64_t o, uint32_t v[4]) {
+    int rn = -1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint64_t p = o + 4 * i;
-        while (p >= en && r + 1 < nrec) {
-            ++r;
-            st = en;
-            en = T.start[r + 1];
-        }
         uint32_t w = 0;
-        if (p >= st && p < en) {
-            const uint32_t k = uint32_t((p - st) >> 2);
-            const uint32_t meta = T.meta[r];
-            const uint32_t hw = meta_hw(meta);
-            if (k < hw) w = hdr_word(T, a, src, r0, r, uint32_t(en - st), meta, k);
-            else w = gload<uint32_t>(src.payload_arena + T.poff[r] + 4ull * (k - hw));
+        if (p >= e.start && p < e.pst) {
+            w = hdr_word(T, a, src, r0, r, uint32_t(e.en - e.start), uint32_t((p - e.start) >> 2));
+        } else if (p >= e.pst && p < e.en) {
+            w = gload<uint32_t>(e.srcbase + p);
+        } else if (p >= e.en) {
+            // first words of the next record (always header: >= 24 B)
+            if (rn < 0) rn = next_rec(T, nrec, r);
+            if (rn < nrec) {
+                const RecEnt& f = T.ent[rn];
+                w = hdr_word(T, a, src, r0, rn, uint32_t(f.en - f.start), uint32_t((p - f.start) >> 2));
+            }
         }
         v[i] = w;
     }
 }
 
-// enc_emit: one 256-thread workgroup per tile of kEmitRecs records.
-//  1. lane per record: plan_record() again (same function as enc_len, so the
-//     lengths agree), one block scan places output bytes and LDS header
-//     words, the record's header words are serialised into LDS, and its
-//     64-byte output granules are claimed in the granule map.
-//  2. the tile's output bytes [T0, T1) are produced in 16-byte aligned
-//     chunks, one chunk per lane per step, stored with global_store_dwordx4
-//     (a wave writes 1 KiB contiguous per instruction). Pure-payload chunks
-//     are one (unaligned) 16-byte load; other chunks assemble stream words
-//     from the LDS header image and the payload arena. Chunks straddling a
-//     tile boundary are written with byte stores of only this tile's bytes.
-__global__ __launch_bounds__(kTile) void enc_emit_kernel(EncArgs a) {
-    __shared__ EmitTile T;
-    __shared__ uint64_t s_wave[kTile / 64];
+__device__ __forceinline__ void store_chunk(uint8_t* out, uint64_t o, uint64_t lo, uint64_t hi, const uint32_t v[4]) {
+    if (lo == o && hi == o + 16) {
+        *reinterpret_cast<uint4*>(out + o) = make_uint4(v[0], v[1], v[2], v[3]);
+    } else {
+        // Tile-boundary or capacity-boundary chunk: only this tile's bytes.
+        for (uint64_t bpos = lo; bpos < hi; ++bpos) {
+            const uint32_t j = uint32_t(bpos - o);
+            out[bpos] = uint8_t(v[j >> 2] >> (8 * (j & 3)));
+        }
+    }
+}
 
-    const int t = threadIdx.x;
-    const uint64_t r0 = uint64_t(blockIdx.x) * kEmitRecs;
+// enc_emit: every wavefront owns one tile of kEmitRecs = 64 records and
+// never waits for another wave (no workgroup barrier), so staging of one
+// wave overlaps the copying of the other waves on the same CU.
+//  Staging (lane per record): plan_record() again (the same function as
+//  enc_len, so lengths agree); a wavefront __shfl scan places output bytes
+//  and LDS header words; each record writes its 32-byte LDS entry,
+//  serialises its header words into LDS and claims its 64-byte output
+//  granules in the granule map. A chunk (16 output bytes, 16-aligned) is
+//  owned by the record holding its first in-tile byte; it is "fast" when it
+//  lies entirely inside its owner's payload, "special" otherwise.
+//  Special pass (lane per record): each record stores its own special
+//  chunks (header words from LDS, boundary bytes) — no search.
+//  Fast pass (lane per chunk): granule map -> record entry -> one unaligned
+//  16-byte load + global_store_dwordx4 (1 KiB contiguous per wave store).
+//  Chunks straddling a tile boundary are written with byte stores of only
+//  this tile's bytes, so tiles never exchange data.
+// kLab != 0 only in tools/emit_lab.hip (bit 0: skip the special pass,
+// bit 1: skip the fast pass).
+template <int kLab>
+__global__ __launch_bounds__(kTile, 8) void enc_emit_kernel_t(EncArgs a) {
+    __shared__ WaveTile s_tiles[kTile / 64];
+
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const uint64_t tile = uint64_t(blockIdx.x) * (kTile / 64) + wv;
+    const uint64_t r0 = tile * kEmitRecs;
+    if (r0 >= a.n) return;
+    WaveTile& T = s_tiles[wv];
     const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
-    const uint64_t tile_base = a.tile_base[blockIdx.x];
+    const uint64_t tile_base = a.tile_base[tile];
     const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena),
                      reinterpret_cast<uintptr_t>(a.payload_arena)};
 
-    onc_msg d;
-    uint64_t len = 0;
-    uint32_t meta = 0, hw = 0;
+    uint64_t len = 0, srcbase = 0;
+    uint32_t hw = 0;
     bool word_aligned = true;
-    if (t < nrec) {
-        d = a.msgs[r0 + t];
-        const RecPlan p = plan_record(d, a.unix);
-        len = p.len;
-        meta = p.meta;
-        hw = len ? meta_hw(meta) : 0;
-        word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((src.payload_arena + d.payload_off) & 3) == 0);
-    }
-    // One scan places both the output bytes and the LDS header words:
-    // (len << 16 | hw); per-tile header words < 128 * 181 < 2^16.
-    uint64_t total;
-    const uint64_t excl = block_excl_scan_u64<kTile>((len << 16) | hw, s_wave, &total);
-    const uint64_t start = tile_base + (excl >> 16);
-    const uint64_t T0 = tile_base;
-    const uint64_t T1 = tile_base + (total >> 16);
-    const uint64_t G0 = T0 >> 6;
-    const uint32_t hoff = uint32_t(excl & 0xFFFFu);
-    if (t < nrec) {
-        T.start[t] = start;
-        T.poff[t] = d.payload_off;
-        T.meta[t] = meta;
-        const bool staged = hoff + hw <= uint32_t(kHdrCap);
-        T.hoff[t] = staged ? hoff : kNotStaged;
-        if (len != 0 && staged) put_header_words(d, uint32_t(len), src, &T.hdr[hoff]);
-        // claim the granules whose first byte lies in this record
-        if (len != 0) {
-            const uint64_t g_hi = min((start + len - 1) >> 6, G0 + kMapCap - 1);
-            for (uint64_t g = (start + 63) >> 6; g <= g_hi; ++g) T.map[g - G0] = uint8_t(t);
+    uint64_t start, en, pst;
+    {
+        onc_msg d;
+        uint32_t meta = 0;
+        if (lane < nrec) {
+            d = a.msgs[r0 + lane];
+            const RecPlan p = plan_record(d, a.unix);
+            len = p.len;
+            meta = p.meta;
+            hw = len ? meta_hw(meta) : 0;
+            word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((src.payload_arena + d.payload_off) & 3) == 0);
         }
-        a.rec_off[r0 + t] = start;
-        if (len != 0 && start + len > a.out_cap) a.status[r0 + t] = ONC_ENC_WRITE_ZERO;
+        // One wave scan places output bytes and LDS header words.
+        const uint64_t v = (len << 16) | hw;
+        const uint64_t incl = wave_incl_scan_u64(v);
+        const uint64_t excl = incl - v;
+        start = tile_base + (excl >> 16);
+        en = start + len;
+        pst = start + 4ull * hw;
+        const uint32_t hoff = uint32_t(excl & 0xFFFFu);
+        if (lane < nrec) {
+            srcbase = src.payload_arena + d.payload_off - pst;
+            T.ent[lane] = RecEnt{start, pst, en, srcbase};
+            T.meta[lane] = meta;
+            const bool staged = hoff + hw <= uint32_t(kHdrCap);
+            T.hoff[lane] = staged ? uint16_t(hoff) : kNone16;
+            if (len != 0 && staged) put_header_words(d, uint32_t(len), src, &T.hdr[hoff]);
+            a.rec_off[r0 + lane] = start;
+            if (len != 0 && en > a.out_cap) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
+        }
     }
-    if (t == 0) {
-        T.start[nrec] = T1;
+    const uint64_t T0 = tile_base;
+    const uint64_t T1 = __shfl(en, nrec - 1, 64);
+    const uint64_t G0 = T0 >> 6;
+    if (lane < nrec && len != 0) {
+        // claim the granules whose first byte lies in this record
+        const uint64_t g_hi = min((en - 1) >> 6, G0 + kMapCap - 1);
+        for (uint64_t g = (start + 63) >> 6; g <= g_hi; ++g) T.map[g - G0] = uint8_t(lane);
+    }
+    if (lane == 0) {
+        T.ent[nrec] = RecEnt{T1, T1, T1, 0};
         if (T0 & 63) T.map[0] = 0;      // granule 0 starts before the tile
     }
-    const bool tile_aligned = __syncthreads_and(word_aligned) && (T0 & 3) == 0;
+    const bool tile_aligned = __all(word_aligned) && (T0 & 3) == 0;
+    wave_lds_sync();
 
     const uint64_t E = min(T1, a.out_cap);
     if (E <= T0) return;
+
+    // Special pass: record `lane`'s chunks [own_lo, A) u [B, own_hi).
+    if (!(kLab & 5) && lane < nrec && len != 0) {
+        const RecEnt e{start, pst, en, srcbase};
+        const uint64_t own_lo = (start == T0) ? (start >> 4) : ((start + 15) >> 4);
+        const uint64_t own_hi = (en + 15) >> 4;
+        const uint64_t A = min((pst + 15) >> 4, own_hi);
+        const uint64_t B = max(en >> 4, A);
+        for (uint64_t c = own_lo; c < own_hi; ++c) {
+            if (c == A) c = B;
+            if (c >= own_hi) break;
+            const uint64_t o = c << 4;
+            if (o >= E) break;
+            uint32_t v[4];
+            if (tile_aligned) aligned_special(T, a, src, r0, nrec, lane, e, o, v);
+            else byte_chunk(&T, &a, &src, r0, nrec, lane, o, v);
+            store_chunk(a.out, o, max(o, T0), min(o + 16, E), v);
+        }
+    }
+
+    // Fast pass: every chunk of the tile; the owners' payload-only chunks.
     const uint64_t c_begin = T0 >> 4;
     const uint64_t c_end = (E + 15) >> 4;
-
-    for (uint64_t c = c_begin + t; c < c_end; c += kTile) {
+    for (uint64_t c = c_begin + lane; c < c_end && !(kLab & 2); c += 64) {
         const uint64_t o = c << 4;
         const uint64_t lo = max(o, T0);
-        const uint64_t hi = min(o + 16, E);
-        const int r = locate(T, nrec, G0, lo);
-        const uint64_t st = T.start[r];
-        const uint64_t en = T.start[r + 1];
-        const uint64_t pst = st + 4ull * meta_hw(T.meta[r]);
-        uint32_t v[4];
-        if (o >= pst && o + 16 <= en) {
-            // Pure payload: one 16-byte copy.
-            load16_unaligned(src.payload_arena + T.poff[r] + (o - pst), v);
-        } else if (tile_aligned) {
-            aligned_chunk(T, a, src, r0, nrec, r, o, v);
-        } else {
-            tile_chunk(T, a, src, r0, r, o, v);
-            if (o + 16 > en && en < T1) {
-                // The chunk runs into the next record of this tile; bytes
-                // outside a record read as 0, so the two parts OR together.
-                const int r2 = locate(T, nrec, G0, en);
-                uint32_t b[4];
-                tile_chunk(T, a, src, r0, r2, o, b);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] |= b[i];
-            }
-        }
-        if (lo == o && hi == o + 16) {
-            *reinterpret_cast<uint4*>(a.out + o) = make_uint4(v[0], v[1], v[2], v[3]);
-        } else {
-            // Tile-boundary or capacity-boundary chunk: only this tile's bytes.
-            for (uint64_t bpos = lo; bpos < hi; ++bpos) {
-                const uint32_t j = uint32_t(bpos - o);
-                a.out[bpos] = uint8_t(v[j >> 2] >> (8 * (j & 3)));
-            }
+        const uint64_t g = (lo >> 6) - G0;
+        int r = g < uint64_t(kMapCap) ? int(T.map[g]) : find_ent(T.ent, nrec, lo);
+        RecEnt e = T.ent[r];
+        while (lo >= e.en && r + 1 < nrec) e = T.ent[++r];
+        if (o >= e.pst && o + 16 <= e.en) {
+            uint32_t v[4];
+            load16_unaligned(e.srcbase + o, v);
+            store_chunk(a.out, o, lo, min(o + 16, E), v);
+        } else if (kLab & 4) {
+            uint32_t v[4];
+            if (tile_aligned) aligned_special(T, a, src, r0, nrec, r, e, o, v);
+            else byte_chunk(&T, &a, &src, r0, nrec, r, o, v);
+            store_chunk(a.out, o, lo, min(o + 16, E), v);
         }
     }
 }
@@ -273,8 +336,8 @@ hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
-    const uint64_t tiles = num_emit_tiles(a.n);
-    hipLaunchKernelGGL(enc_emit_kernel, dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
+    const uint64_t blocks = (num_emit_tiles(a.n) + kTile / 64 - 1) / (kTile / 64);
+    hipLaunchKernelGGL(enc_emit_kernel_t<0>, dim3(uint32_t(blocks)), dim3(kTile), 0, s, a);
     return hipGetLastError();
 }
 

@@ -1,0 +1,319 @@
+// emit_lab.hip — A/B timing harness for encode-emit kernel variants (dev tool).
+//
+// Builds the configs[1] workload (1M x Call(AuthNone x2) + 256 B payload)
+// on the device, runs the product pipeline (enc_len -> scan -> enc_emit) as
+// the reference output, then times experimental emit variants interleaved
+// in one process (MI355X guide §5.4 rule 24) and checks each variant's
+// bytes against the product output.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/emit_lab.hip -o tools/emit_lab
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <functional>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "../onc-rpc_amd/csrc/encode.hip"
+#include "../onc-rpc_amd/csrc/scan.hip"
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+using namespace onc;
+
+// ---- V_copy: ideal 16-byte grid-stride copy of the output size ----------
+__global__ __launch_bounds__(256) void v_copy(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n16) {
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * 256)
+        out[i] = in[i];
+}
+
+// ---- V_fixed: configs[1]-only structured copy (record = arithmetic) -------
+// Header chunks use the same word logic from registers; measures the cost
+// of the record structure without any LDS/search machinery.
+__global__ __launch_bounds__(256) void v_fixed(const uint8_t* __restrict__ payload, uint8_t* __restrict__ out,
+                                               uint64_t n, uint32_t W, uint32_t H) {
+    const uint64_t total = n * W;
+    const uint64_t n16 = (total + 15) / 16;
+    for (uint64_t c = uint64_t(blockIdx.x) * 256 + threadIdx.x; c < n16; c += uint64_t(gridDim.x) * 256) {
+        const uint64_t o = c * 16;
+        const uint64_t r = o / W;
+        const uint64_t st = r * W, pst = st + H, en = st + W;
+        uint32_t v[4];
+        if (o >= pst && o + 16 <= en) {
+            load16_unaligned(reinterpret_cast<uintptr_t>(payload) + r * (W - H) + (o - pst), v);
+        } else {
+            v[0] = v[1] = v[2] = v[3] = 0;
+        }
+        if (o + 16 <= total) *reinterpret_cast<uint4*>(out + o) = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+// ---- V_rec<K>: record-driven copy, K lanes per record (configs[1] shape) --
+template <int K>
+__global__ __launch_bounds__(256) void v_rec(const uint8_t* __restrict__ payload, uint8_t* __restrict__ out,
+                                             uint64_t n, uint32_t W, uint32_t H) {
+    const uint64_t lane_rec = (uint64_t(blockIdx.x) * 256 + threadIdx.x) / K;
+    const uint32_t sub = threadIdx.x % K;
+    const uint64_t stride = uint64_t(gridDim.x) * 256 / K;
+    for (uint64_t r = lane_rec; r < n; r += stride) {
+        const uint64_t st = r * W, pst = st + H, en = st + W;
+        const uint64_t A = (pst + 15) >> 4, B = en >> 4;
+        const uintptr_t sb = reinterpret_cast<uintptr_t>(payload) + r * (W - H) - pst;
+        for (uint64_t c = A + sub; c < B; c += K) {
+            uint32_t v[4];
+            load16_unaligned(sb + (c << 4), v);
+            *reinterpret_cast<uint4*>(out + (c << 4)) = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+    }
+}
+
+// ---- V_lds: product fast-pass lookups, arithmetic staging (configs[1]) ---
+template <int kWaves, int U = 1>
+__global__ __launch_bounds__(64 * kWaves) void v_lds(const uint8_t* __restrict__ payload, uint8_t* __restrict__ out,
+                                                     uint64_t n, uint32_t W, uint32_t H) {
+    __shared__ RecEnt s_ent[kWaves][65];
+    __shared__ uint8_t s_map[kWaves][512];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t tile = uint64_t(blockIdx.x) * kWaves + wv;
+    const uint64_t r0 = tile * 64;
+    if (r0 >= n) return;
+    const int nrec = int(min(uint64_t(64), n - r0));
+    RecEnt* ent = s_ent[wv];
+    uint8_t* map = s_map[wv];
+    const uint64_t T0 = r0 * W, T1 = (r0 + nrec) * W, G0 = T0 >> 6;
+    if (lane < nrec) {
+        const uint64_t r = r0 + lane, st = r * W, pst = st + H, en = st + W;
+        ent[lane] = RecEnt{st, pst, en, reinterpret_cast<uintptr_t>(payload) + r * (W - H) - pst};
+        const uint64_t g_hi = min((en - 1) >> 6, G0 + 511);
+        for (uint64_t g = (st + 63) >> 6; g <= g_hi; ++g) map[g - G0] = uint8_t(lane);
+    }
+    if (lane == 0) {
+        ent[nrec] = RecEnt{T1, T1, T1, 0};
+        if (T0 & 63) map[0] = 0;
+    }
+    wave_lds_sync();
+    const uint64_t c_begin = T0 >> 4, c_end = (T1 + 15) >> 4;
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(payload);
+    for (uint64_t cb = c_begin + lane; cb < c_end; cb += 64 * U) {
+        uintptr_t addr[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t c = cb + 64 * u;
+            const uint64_t o = c << 4;
+            const uint64_t lo = max(o, T0);
+            const uint64_t g = min((lo >> 6) - G0, uint64_t(511));
+            int r = map[g];
+            RecEnt e = ent[r];
+            if (lo >= e.en && r + 1 < nrec) e = ent[++r];
+            ok[u] = c < c_end && o >= e.pst && o + 16 <= e.en;
+            addr[u] = ok[u] ? e.srcbase + o : dummy;
+        }
+        uint32_t v[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) load16_unaligned(addr[u], v[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (ok[u]) *reinterpret_cast<uint4*>(out + ((cb + 64 * u) << 4)) = make_uint4(v[u][0], v[u][1], v[u][2], v[u][3]);
+    }
+}
+
+// ---- V_fixed_tiled: arithmetic lookup, but each wave owns a 64-record tile
+template <bool kAll>
+__global__ __launch_bounds__(256) void v_fixed_tiled(const uint8_t* __restrict__ payload, uint8_t* __restrict__ out,
+                                                     uint64_t n, uint32_t W, uint32_t H, uint32_t recs_per_wave) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t tile = (uint64_t(blockIdx.x) * 256 + threadIdx.x) / 64;
+    const uint64_t r0 = tile * recs_per_wave;
+    if (r0 >= n) return;
+    const uint64_t T0 = r0 * W, T1 = min(n, r0 + recs_per_wave) * W;
+    for (uint64_t c = (T0 >> 4) + lane; c < (T1 + 15) >> 4; c += 64) {
+        const uint64_t o = c * 16;
+        const uint64_t r = o / W;
+        const uint64_t st = r * W, pst = st + H, en = st + W;
+        uint32_t v[4] = {0, 0, 0, 0};
+        const bool fast = o >= pst && o + 16 <= en;
+        if (fast) load16_unaligned(reinterpret_cast<uintptr_t>(payload) + r * (W - H) + (o - pst), v);
+        if (fast || kAll) *reinterpret_cast<uint4*>(out + o) = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+// ---- V_fixed_blocktiled: block of B threads owns R records, sweeps B*16 B per step
+template <int B>
+__global__ __launch_bounds__(B) void v_fixed_blocktiled(const uint8_t* __restrict__ payload, uint8_t* __restrict__ out,
+                                                        uint64_t n, uint32_t W, uint32_t H, uint32_t R) {
+    const uint64_t r0 = uint64_t(blockIdx.x) * R;
+    if (r0 >= n) return;
+    const uint64_t T0 = r0 * W, T1 = min(n, r0 + R) * W;
+    for (uint64_t c = (T0 >> 4) + threadIdx.x; c < (T1 + 15) >> 4; c += B) {
+        const uint64_t o = c * 16;
+        const uint64_t r = o / W;
+        const uint64_t st = r * W, pst = st + H, en = st + W;
+        if (o >= pst && o + 16 <= en) {
+            uint32_t v[4];
+            load16_unaligned(reinterpret_cast<uintptr_t>(payload) + r * (W - H) + (o - pst), v);
+            *reinterpret_cast<uint4*>(out + o) = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+    }
+}
+
+// ---- V_fixed_persist: persistent waves, wave-owned R-record tiles, tile
+// index strided by the number of waves in the grid
+__global__ __launch_bounds__(256) void v_fixed_persist(const uint8_t* __restrict__ payload, uint8_t* __restrict__ out,
+                                                       uint64_t n, uint32_t W, uint32_t H, uint32_t R) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = uint64_t(gridDim.x) * 4;
+    for (uint64_t tile = (uint64_t(blockIdx.x) * 256 + threadIdx.x) / 64; tile * R < n; tile += nw) {
+        const uint64_t r0 = tile * R;
+        const uint64_t T0 = r0 * W, T1 = min(n, r0 + R) * W;
+        for (uint64_t c = (T0 >> 4) + lane; c < (T1 + 15) >> 4; c += 64) {
+            const uint64_t o = c * 16;
+            const uint64_t r = o / W;
+            const uint64_t st = r * W, pst = st + H, en = st + W;
+            if (o >= pst && o + 16 <= en) {
+                uint32_t v[4];
+                load16_unaligned(reinterpret_cast<uintptr_t>(payload) + r * (W - H) + (o - pst), v);
+                *reinterpret_cast<uint4*>(out + o) = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    }
+}
+
+int main(int argc, char** argv) {
+    const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1000000;
+    const uint32_t P = 256, H = 44, W = H + P;
+    std::vector<onc_msg> msgs(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        onc_msg& m = msgs[i];
+        memset(&m, 0, sizeof(m));
+        m.xid = uint32_t(i);
+        m.msg_type = ONC_MSG_CALL;
+        m.u.call.program = 100003;
+        m.u.call.program_version = 4;
+        m.u.call.procedure = 1;
+        m.payload_len = P;
+        m.payload_off = i * P;
+        m.cred.kind_len = ONC_AUTH_PACK(ONC_KIND_NONE, 0);
+        m.verf.kind_len = ONC_AUTH_PACK(ONC_KIND_NONE, 0);
+    }
+    std::vector<uint8_t> pay(n * P + 16);
+    std::mt19937_64 rng(1);
+    for (auto& b : pay) b = uint8_t(rng());
+
+    onc_msg* d_msgs;
+    uint8_t *d_pay, *d_out, *d_out2, *d_auth;
+    onc_unix_params* d_unix;
+    uint64_t *d_off, *d_scr;
+    int32_t* d_st;
+    const uint64_t tiles = num_emit_tiles(n);
+    CK(hipMalloc(&d_msgs, n * sizeof(onc_msg)));
+    CK(hipMalloc(&d_pay, pay.size()));
+    CK(hipMalloc(&d_out, n * W + 64));
+    CK(hipMalloc(&d_out2, n * W + 64));
+    CK(hipMalloc(&d_auth, 64));
+    CK(hipMalloc(&d_unix, sizeof(onc_unix_params)));
+    CK(hipMalloc(&d_off, (n + 1) * 8));
+    CK(hipMalloc(&d_scr, 2 * tiles * 8 + 64));
+    CK(hipMalloc(&d_st, n * 4));
+    CK(hipMemcpy(d_msgs, msgs.data(), n * sizeof(onc_msg), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_pay, pay.data(), pay.size(), hipMemcpyHostToDevice));
+
+    EncArgs a{};
+    a.n = n;
+    a.msgs = d_msgs;
+    a.unix = d_unix;
+    a.auth_arena = d_auth;
+    a.payload_arena = d_pay;
+    a.out = d_out;
+    a.out_cap = n * W;
+    a.rec_off = d_off;
+    a.status = d_st;
+    a.tile_sum = d_scr;
+    a.tile_base = d_scr + tiles;
+    CK(launch_enc_len(a, 0));
+    CK(launch_scan_tiles(a.tile_sum, d_scr + tiles, tiles, 0, d_off + n, 0));
+    CK(launch_enc_emit(a, 0));
+    CK(hipDeviceSynchronize());
+    std::vector<uint8_t> ref(n * W);
+    CK(hipMemcpy(ref.data(), d_out, n * W, hipMemcpyDeviceToHost));
+
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    struct Var {
+        const char* name;
+        bool check;
+        std::function<void()> run;
+    };
+    EncArgs a2 = a;
+    a2.out = d_out2;
+    const uint64_t n16 = (n * W + 15) / 16;
+    std::vector<Var> vars = {
+        {"product_emit", true, [&] { launch_enc_emit(a2, 0); }},
+        {"copy_256MB_payload_ideal", false,
+         [&] { hipLaunchKernelGGL(v_copy, dim3(2048), dim3(256), 0, 0, (const uint4*)d_pay, (uint4*)d_out2, n * P / 16); }},
+        {"fixed_structured_copy", false,
+         [&] { hipLaunchKernelGGL(v_fixed, dim3(2048), dim3(256), 0, 0, d_pay, d_out2, n, W, H); }},
+        {"product_len", false, [&] { launch_enc_len(a2, 0); }},
+        {"lds_lookup_copy_4w", false, [&] { hipLaunchKernelGGL(v_lds<4>, dim3((tiles + 3) / 4), dim3(256), 0, 0, d_pay, d_out2, n, W, H); }},
+        
+        
+        {"fixed_tiled_64rec_all_stores", false, [&] { hipLaunchKernelGGL(v_fixed_tiled<true>, dim3((n / 64 + 4) / 4), dim3(256), 0, 0, d_pay, d_out2, n, W, H, 64u); }},
+        {"fixed_tiled_64rec", false, [&] { hipLaunchKernelGGL(v_fixed_tiled<false>, dim3((n / 64 + 4) / 4), dim3(256), 0, 0, d_pay, d_out2, n, W, H, 64u); }},
+        
+        {"fixed_tiled_4rec", false, [&] { hipLaunchKernelGGL(v_fixed_tiled<false>, dim3((n / 4 + 4) / 4), dim3(256), 0, 0, d_pay, d_out2, n, W, H, 4u); }},
+        {"blocktiled_256thr_256rec", false, [&] { hipLaunchKernelGGL(v_fixed_blocktiled<256>, dim3((n + 255) / 256), dim3(256), 0, 0, d_pay, d_out2, n, W, H, 256u); }},
+        
+        
+        
+        {"persist_64rec", false, [&] { hipLaunchKernelGGL(v_fixed_persist, dim3(2048), dim3(256), 0, 0, d_pay, d_out2, n, W, H, 64u); }},
+        {"persist_16rec", false, [&] { hipLaunchKernelGGL(v_fixed_persist, dim3(2048), dim3(256), 0, 0, d_pay, d_out2, n, W, H, 16u); }},
+        
+        
+        
+        {"rec_copy_16lanes", false, [&] { hipLaunchKernelGGL(v_rec<16>, dim3(2048), dim3(256), 0, 0, d_pay, d_out2, n, W, H); }},
+        {"emit_single_pass", true, [&] { hipLaunchKernelGGL(enc_emit_kernel_t<4>, dim3((tiles + 3) / 4), dim3(kTile), 0, 0, a2); }},
+        {"emit_no_pass2", false, [&] { hipLaunchKernelGGL(enc_emit_kernel_t<1>, dim3((tiles + 3) / 4), dim3(kTile), 0, 0, a2); }},
+        {"emit_no_pass1", false, [&] { hipLaunchKernelGGL(enc_emit_kernel_t<2>, dim3((tiles + 3) / 4), dim3(kTile), 0, 0, a2); }},
+        {"emit_staging_only", false, [&] { hipLaunchKernelGGL(enc_emit_kernel_t<3>, dim3((tiles + 3) / 4), dim3(kTile), 0, 0, a2); }},
+    };
+    const int reps = 10, rounds = 5;
+    std::vector<std::vector<float>> times(vars.size());
+    for (int round = 0; round < rounds; ++round) {
+        for (size_t v = 0; v < vars.size(); ++v) {
+            vars[v].run();  // warm
+            CK(hipEventRecord(e0, 0));
+            for (int i = 0; i < reps; ++i) vars[v].run();
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            times[v].push_back(ms * 1000.f / reps);
+        }
+    }
+    for (size_t v = 0; v < vars.size(); ++v) {
+        auto t = times[v];
+        std::sort(t.begin(), t.end());
+        bool ok = true;
+        if (vars[v].check) {
+            CK(hipMemset(d_out2, 0, n * W));
+            vars[v].run();
+            CK(hipDeviceSynchronize());
+            std::vector<uint8_t> got(n * W);
+            CK(hipMemcpy(got.data(), d_out2, n * W, hipMemcpyDeviceToHost));
+            ok = got == ref;
+        }
+        printf("%-28s median %8.1f us  min %8.1f us  %s\n", vars[v].name, t[t.size() / 2], t[0],
+               vars[v].check ? (ok ? "bit-exact" : "MISMATCH") : "-");
+    }
+    return 0;
+}
