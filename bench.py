@@ -209,6 +209,7 @@ def main():
         "decode_kernel": 2 * H + 4,        # zero-copy decode
         "len_tiles_kernel": 4,
         "len_apply_kernel": 12,
+        "enc_fixup_kernel": 0,             # deferred tiles only (none for this workload)
     }
     kern = {}
     for name, (tot_ms, cnt) in kstats.items():

@@ -247,7 +247,8 @@ int onc_abi_version(void);
 #define ONC_K_DEC_PARSE   3
 #define ONC_K_LEN_TILES   4
 #define ONC_K_LEN_APPLY   5
-#define ONC_K_COUNT       6
+#define ONC_K_ENC_FIXUP   6
+#define ONC_K_COUNT       7
 int onc_codec_enable_timing(onc_codec* codec, int enable);
 int onc_codec_kernel_stats(onc_codec* codec, double* ms_total /*[ONC_K_COUNT]*/,
                            uint64_t* launches /*[ONC_K_COUNT]*/);

@@ -15,7 +15,8 @@
 struct onc_codec {
     int device = 0;
     hipStream_t stream = nullptr;
-    uint64_t* scratch = nullptr;   // [tile_sum | tile_base], 2 * scratch_tiles entries
+    // [tile_sum | tile_base | defer_list (u32) | defer_count], 3 * scratch_tiles + 2 u64 entries
+    uint64_t* scratch = nullptr;
     uint64_t scratch_tiles = 0;
     bool timing = false;
     struct Pending {
@@ -78,7 +79,7 @@ int ensure_scratch(onc_codec* c, uint64_t tiles) {
         c->scratch = nullptr;
         c->scratch_tiles = 0;
     }
-    hipError_t e = hipMalloc(&c->scratch, 2 * want * sizeof(uint64_t));
+    hipError_t e = hipMalloc(&c->scratch, (3 * want + 2) * sizeof(uint64_t));
     if (e != hipSuccess) {
         fail(c, e, "hipMalloc(scratch)");
         return ONC_RC_ENOMEM;
@@ -185,6 +186,7 @@ const char* onc_kernel_name(int k) {
         case ONC_K_DEC_PARSE: return "decode_kernel";
         case ONC_K_LEN_TILES: return "len_tiles_kernel";
         case ONC_K_LEN_APPLY: return "len_apply_kernel";
+        case ONC_K_ENC_FIXUP: return "enc_fixup_kernel";
         default: return "?";
     }
 }
@@ -251,6 +253,7 @@ int onc_encode_lengths(onc_codec* c, const onc_batch* batch, uint32_t* rec_len, 
     a.status = status;
     a.rec_len = rec_len;
     a.tile_sum = c->scratch;
+    a.defer_count = reinterpret_cast<uint32_t*>(c->scratch + 3 * c->scratch_tiles);
     return run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
 }
 
@@ -280,6 +283,8 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
     a.rec_len = rec_len;
     a.tile_sum = c->scratch;
     a.tile_base = c->scratch + c->scratch_tiles;
+    a.defer_list = reinterpret_cast<uint32_t*>(c->scratch + 2 * c->scratch_tiles);
+    a.defer_count = reinterpret_cast<uint32_t*>(c->scratch + 3 * c->scratch_tiles);
     rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
     rc = run(c, ONC_K_SCAN_TILES, "scan_tiles", [&] {
@@ -287,7 +292,9 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
                                       c->stream);
     });
     if (rc != ONC_RC_OK) return rc;
-    return run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
+    rc = run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    return run(c, ONC_K_ENC_FIXUP, "enc_fixup", [&] { return onc::launch_enc_fixup(a, c->stream); });
 }
 
 int onc_decode(onc_codec* c, const uint8_t* wire, const uint64_t* rec_off, uint64_t n, int mode,

@@ -42,6 +42,7 @@ __global__ __launch_bounds__(kTile) void enc_len_kernel(EncArgs a) {
     const uint64_t incl = wave_incl_scan_u64(len);
     const uint64_t tile = r / kEmitRecs;
     if ((threadIdx.x & 63) == 63 && tile * kEmitRecs < a.n) a.tile_sum[tile] = incl;
+    if (r == 0) *a.defer_count = 0;   // enc_emit appends to the deferred-tile list
 }
 
 // Largest r in [0, nrec) with start[r] <= x (start ascending). Records of
@@ -202,130 +203,227 @@ __device__ __forceinline__ void store_chunk(uint8_t* out, uint64_t o, uint64_t l
     }
 }
 
+// enc_fixup: the tiles enc_emit deferred (a record that is not 4-byte
+// aligned — unpadded odd-length payloads — or headers beyond the fast
+// kernel's LDS budget). One wavefront per tile, single chunk pass: every
+// chunk (payload-only or special) is computed by its lane and all chunks of
+// a step are stored by one global_store_dwordx4, so 128-byte lines are
+// always written whole.
+__global__ __launch_bounds__(kTile) void enc_fixup_kernel(EncArgs a) {
+    __shared__ WaveTile s_tiles[kTile / 64];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    WaveTile& T = s_tiles[wv];
+    const uint32_t ndef = *a.defer_count;
+    const uint64_t nwaves = uint64_t(gridDim.x) * (kTile / 64);
+    const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena),
+                     reinterpret_cast<uintptr_t>(a.payload_arena)};
+    for (uint64_t i = uint64_t(blockIdx.x) * (kTile / 64) + wv; i < ndef; i += nwaves) {
+        const uint64_t tile = a.defer_list[i];
+        const uint64_t r0 = tile * kEmitRecs;
+        const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
+        const uint64_t tile_base = a.tile_base[tile];
+        wave_lds_sync();   // the previous tile's readers are done with T
+
+        uint64_t len = 0, srcbase = 0;
+        uint32_t hw = 0;
+        bool word_aligned = true;
+        uint64_t start, en, pst;
+        {
+            onc_msg d;
+            uint32_t meta = 0;
+            if (lane < nrec) {
+                d = a.msgs[r0 + lane];
+                const RecPlan p = plan_record(d, a.unix);
+                len = p.len;
+                meta = p.meta;
+                hw = len ? meta_hw(meta) : 0;
+                word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((src.payload_arena + d.payload_off) & 3) == 0);
+            }
+            const uint64_t v = (len << 16) | hw;
+            const uint64_t incl = wave_incl_scan_u64(v);
+            const uint64_t excl = incl - v;
+            start = tile_base + (excl >> 16);
+            en = start + len;
+            pst = start + 4ull * hw;
+            const uint32_t hoff = uint32_t(excl & 0xFFFFu);
+            if (lane < nrec) {
+                srcbase = src.payload_arena + d.payload_off - pst;
+                T.ent[lane] = RecEnt{start, pst, en, srcbase};
+                T.meta[lane] = meta;
+                const bool staged = hoff + hw <= uint32_t(kHdrCap);
+                T.hoff[lane] = staged ? uint16_t(hoff) : kNone16;
+                if (len != 0 && staged) put_header_words(d, uint32_t(len), src, &T.hdr[hoff]);
+            }
+        }
+        const uint64_t T0 = tile_base;
+        const uint64_t T1 = __shfl(en, nrec - 1, 64);
+        const uint64_t G0 = T0 >> 6;
+        if (lane < nrec && len != 0) {
+            const uint64_t g_hi = min((en - 1) >> 6, G0 + kMapCap - 1);
+            for (uint64_t g = (start + 63) >> 6; g <= g_hi; ++g) T.map[g - G0] = uint8_t(lane);
+        }
+        if (lane == 0) {
+            T.ent[nrec] = RecEnt{T1, T1, T1, 0};
+            if (T0 & 63) T.map[0] = 0;
+        }
+        const bool tile_aligned = __all(word_aligned) && (T0 & 3) == 0;
+        wave_lds_sync();
+
+        const uint64_t E = min(T1, a.out_cap);
+        if (E <= T0) continue;
+        for (uint64_t c = (T0 >> 4) + lane; c < (E + 15) >> 4; c += 64) {
+            const uint64_t o = c << 4;
+            const uint64_t lo = max(o, T0);
+            const uint64_t g = (lo >> 6) - G0;
+            int r = g < uint64_t(kMapCap) ? int(T.map[g]) : find_ent(T.ent, nrec, lo);
+            RecEnt e = T.ent[r];
+            while (lo >= e.en && r + 1 < nrec) e = T.ent[++r];
+            uint32_t v[4];
+            if (o >= e.pst && o + 16 <= e.en) load16_unaligned(e.srcbase + o, v);
+            else if (tile_aligned) aligned_special(T, a, src, r0, nrec, r, e, o, v);
+            else byte_chunk(&T, &a, &src, r0, nrec, r, o, v);
+            store_chunk(a.out, o, lo, min(o + 16, E), v);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// enc_emit: the hot kernel.
+// ---------------------------------------------------------------------------
+constexpr int kFastHdrCap = 1024;             // header words per wave tile (4 KiB of LDS)
+constexpr int kFastMapCap = 1024;             // output granules per wave tile
+
+// Per-record LDS entry of the fast kernel (two ds_read_b128).
+struct FastEnt {
+    uint64_t pst;       // first payload byte
+    uint64_t en;        // one past the last byte
+    uint64_t srcbase;   // payload byte at output offset o lives at srcbase + o
+    int32_t dw;         // LDS header word of the output dword at p: ((p - T0) >> 2) + dw
+    int32_t dwn;        // the same for the next record
+};
+
+struct FastTile {
+    FastEnt ent[kEmitRecs + 1];      // [nrec] = sentinel {T1, T1, 0, 0, 0}
+    uint32_t hdr[kFastHdrCap];       // header words of the tile's records (stream order)
+    uint8_t map[kFastMapCap];        // granule -> record holding its first in-tile byte
+};
+
 // enc_emit: every wavefront owns one tile of kEmitRecs = 64 records and
-// never waits for another wave (no workgroup barrier), so staging of one
-// wave overlaps the copying of the other waves on the same CU.
+// never waits for another wave (no workgroup barrier), so the staging of one
+// wave overlaps the streaming of the others on the same CU.
 //  Staging (lane per record): plan_record() again (the same function as
-//  enc_len, so lengths agree); a wavefront __shfl scan places output bytes
-//  and LDS header words; each record writes its 32-byte LDS entry,
-//  serialises its header words into LDS and claims its 64-byte output
-//  granules in the granule map. A chunk (16 output bytes, 16-aligned) is
-//  owned by the record holding its first in-tile byte; it is "fast" when it
-//  lies entirely inside its owner's payload, "special" otherwise.
-//  Special pass (lane per record): each record stores its own special
-//  chunks (header words from LDS, boundary bytes) — no search.
-//  Fast pass (lane per chunk): granule map -> record entry -> one unaligned
-//  16-byte load + global_store_dwordx4 (1 KiB contiguous per wave store).
+//  enc_len, so lengths agree); one wavefront __shfl scan places output
+//  bytes and LDS header words; each record writes its LDS entry, serialises
+//  its header words into LDS, and claims its output granules in the
+//  granule map (granule = 64 B, doubled until the tile fits the map).
+//  Tiles whose records are not all 4-byte aligned, or whose headers exceed
+//  the LDS budget, are appended to the deferred list for enc_fixup.
+//  Chunk pass (lane per 16-byte output chunk, 1 KiB contiguous per wave):
+//  granule map -> record entry; a chunk inside its record's payload is one
+//  unaligned 16-byte load; any other chunk takes each of its four dwords
+//  from the LDS header image (this record's or the next one's header) or
+//  the payload. Every chunk of a step, payload-only or not, is stored by the
+//  same global_store_dwordx4, so 128-byte lines are always written whole
+//  (a line left partially written costs a read-modify-write at eviction).
 //  Chunks straddling a tile boundary are written with byte stores of only
 //  this tile's bytes, so tiles never exchange data.
-// kLab != 0 only in tools/emit_lab.hip (bit 0: skip the special pass,
-// bit 1: skip the fast pass).
+// kLab != 0 only in tools/emit_lab.hip.
 template <int kLab>
-__global__ __launch_bounds__(kTile, 8) void enc_emit_kernel_t(EncArgs a) {
-    __shared__ WaveTile s_tiles[kTile / 64];
+__global__ __launch_bounds__(kTile) void enc_emit_kernel_t(EncArgs a) {
+    __shared__ FastTile s_tiles[kTile / 64];
 
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const uint64_t tile = uint64_t(blockIdx.x) * (kTile / 64) + wv;
     const uint64_t r0 = tile * kEmitRecs;
     if (r0 >= a.n) return;
-    WaveTile& T = s_tiles[wv];
+    FastTile& T = s_tiles[wv];
     const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
-    const uint64_t tile_base = a.tile_base[tile];
-    const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena),
-                     reinterpret_cast<uintptr_t>(a.payload_arena)};
+    const uint64_t T0 = a.tile_base[tile];
+    const uintptr_t payload = reinterpret_cast<uintptr_t>(a.payload_arena);
 
-    uint64_t len = 0, srcbase = 0;
-    uint32_t hw = 0;
+    onc_msg d;
+    uint64_t len = 0;
+    uint32_t meta = 0, hw = 0;
     bool word_aligned = true;
-    uint64_t start, en, pst;
-    {
-        onc_msg d;
-        uint32_t meta = 0;
-        if (lane < nrec) {
-            d = a.msgs[r0 + lane];
-            const RecPlan p = plan_record(d, a.unix);
-            len = p.len;
-            meta = p.meta;
-            hw = len ? meta_hw(meta) : 0;
-            word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((src.payload_arena + d.payload_off) & 3) == 0);
-        }
-        // One wave scan places output bytes and LDS header words.
-        const uint64_t v = (len << 16) | hw;
-        const uint64_t incl = wave_incl_scan_u64(v);
-        const uint64_t excl = incl - v;
-        start = tile_base + (excl >> 16);
-        en = start + len;
-        pst = start + 4ull * hw;
-        const uint32_t hoff = uint32_t(excl & 0xFFFFu);
-        if (lane < nrec) {
-            srcbase = src.payload_arena + d.payload_off - pst;
-            T.ent[lane] = RecEnt{start, pst, en, srcbase};
-            T.meta[lane] = meta;
-            const bool staged = hoff + hw <= uint32_t(kHdrCap);
-            T.hoff[lane] = staged ? uint16_t(hoff) : kNone16;
-            if (len != 0 && staged) put_header_words(d, uint32_t(len), src, &T.hdr[hoff]);
-            a.rec_off[r0 + lane] = start;
-            if (len != 0 && en > a.out_cap) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
+    if (lane < nrec) {
+        d = a.msgs[r0 + lane];
+        const RecPlan p = plan_record(d, a.unix);
+        len = p.len;
+        meta = p.meta;
+        hw = len ? meta_hw(meta) : 0;
+        word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((payload + d.payload_off) & 3) == 0);
+    }
+    // One wave scan places output bytes and LDS header words: (len << 16 | hw).
+    const uint64_t sv = (len << 16) | hw;
+    const uint64_t incl = wave_incl_scan_u64(sv);
+    const uint64_t excl = incl - sv;
+    const uint64_t start = T0 + (excl >> 16);
+    const uint64_t en = start + len;
+    const uint64_t pst = start + 4ull * hw;
+    const uint32_t hoff = uint32_t(excl & 0xFFFFu);
+    const uint64_t last = __shfl(incl, nrec - 1, 64);
+    const uint64_t T1 = T0 + (last >> 16);
+    if (lane < nrec) {
+        a.rec_off[r0 + lane] = start;
+        if (len != 0 && en > a.out_cap) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
+    }
+    const bool fast = __all(word_aligned) && (T0 & 3) == 0 && (last & 0xFFFFu) <= uint64_t(kFastHdrCap);
+    if (!fast) {
+        if (lane == 0) a.defer_list[atomicAdd(a.defer_count, 1u)] = uint32_t(tile);
+        return;
+    }
+    const int32_t dw = int32_t(hoff) - int32_t((start - T0) >> 2);
+    const int32_t dwn_raw = __shfl_down(dw, 1, 64);
+    if (lane < nrec) {
+        const uint64_t srcbase = payload + d.payload_off - pst;
+        T.ent[lane] = FastEnt{pst, en, srcbase, dw, lane + 1 < nrec ? dwn_raw : dw};
+        if (len != 0) {
+            const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
+            put_header_words(d, uint32_t(len), src, &T.hdr[hoff]);
         }
     }
-    const uint64_t T0 = tile_base;
-    const uint64_t T1 = __shfl(en, nrec - 1, 64);
-    const uint64_t G0 = T0 >> 6;
+    // granule size: 64 B, doubled until the tile's bytes fit the map
+    uint32_t gs = 6;
+    while (((T1 - T0) >> gs) >= uint64_t(kFastMapCap)) ++gs;
+    const uint64_t G0 = T0 >> gs;
     if (lane < nrec && len != 0) {
         // claim the granules whose first byte lies in this record
-        const uint64_t g_hi = min((en - 1) >> 6, G0 + kMapCap - 1);
-        for (uint64_t g = (start + 63) >> 6; g <= g_hi; ++g) T.map[g - G0] = uint8_t(lane);
+        const uint64_t gsz = 1ull << gs;
+        for (uint64_t g = (start + gsz - 1) >> gs; g <= (en - 1) >> gs; ++g) T.map[g - G0] = uint8_t(lane);
     }
     if (lane == 0) {
-        T.ent[nrec] = RecEnt{T1, T1, T1, 0};
-        if (T0 & 63) T.map[0] = 0;      // granule 0 starts before the tile
+        T.ent[nrec] = FastEnt{T1, T1, 0, 0, 0};
+        if (T0 & ((1ull << gs) - 1)) T.map[0] = 0;   // granule 0 starts before the tile
     }
-    const bool tile_aligned = __all(word_aligned) && (T0 & 3) == 0;
     wave_lds_sync();
 
     const uint64_t E = min(T1, a.out_cap);
-    if (E <= T0) return;
-
-    // Special pass: record `lane`'s chunks [own_lo, A) u [B, own_hi).
-    if (!(kLab & 5) && lane < nrec && len != 0) {
-        const RecEnt e{start, pst, en, srcbase};
-        const uint64_t own_lo = (start == T0) ? (start >> 4) : ((start + 15) >> 4);
-        const uint64_t own_hi = (en + 15) >> 4;
-        const uint64_t A = min((pst + 15) >> 4, own_hi);
-        const uint64_t B = max(en >> 4, A);
-        for (uint64_t c = own_lo; c < own_hi; ++c) {
-            if (c == A) c = B;
-            if (c >= own_hi) break;
-            const uint64_t o = c << 4;
-            if (o >= E) break;
-            uint32_t v[4];
-            if (tile_aligned) aligned_special(T, a, src, r0, nrec, lane, e, o, v);
-            else byte_chunk(&T, &a, &src, r0, nrec, lane, o, v);
-            store_chunk(a.out, o, max(o, T0), min(o + 16, E), v);
-        }
-    }
-
-    // Fast pass: every chunk of the tile; the owners' payload-only chunks.
-    const uint64_t c_begin = T0 >> 4;
-    const uint64_t c_end = (E + 15) >> 4;
-    for (uint64_t c = c_begin + lane; c < c_end && !(kLab & 2); c += 64) {
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.msgs);   // >= 64 valid bytes
+    for (uint64_t c = (T0 >> 4) + lane; c < (E + 15) >> 4; c += 64) {
         const uint64_t o = c << 4;
         const uint64_t lo = max(o, T0);
-        const uint64_t g = (lo >> 6) - G0;
-        int r = g < uint64_t(kMapCap) ? int(T.map[g]) : find_ent(T.ent, nrec, lo);
-        RecEnt e = T.ent[r];
-        while (lo >= e.en && r + 1 < nrec) e = T.ent[++r];
+        int r = T.map[(lo >> gs) - G0];
+        FastEnt e = T.ent[r];
+        while (lo >= e.en) e = T.ent[++r];            // sentinel en = T1 > lo
+        uint32_t v[4];
         if (o >= e.pst && o + 16 <= e.en) {
-            uint32_t v[4];
             load16_unaligned(e.srcbase + o, v);
-            store_chunk(a.out, o, lo, min(o + 16, E), v);
-        } else if (kLab & 4) {
-            uint32_t v[4];
-            if (tile_aligned) aligned_special(T, a, src, r0, nrec, r, e, o, v);
-            else byte_chunk(&T, &a, &src, r0, nrec, r, o, v);
-            store_chunk(a.out, o, lo, min(o + 16, E), v);
+        } else {
+            const int64_t q = (int64_t(o) - int64_t(T0)) >> 2;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint64_t p = o + 4 * i;
+                const bool in_pay = p >= e.pst && p < e.en;
+                const int64_t hidx = q + i + (p >= e.en ? e.dwn : e.dw);
+                const int64_t hcl = hidx < 0 ? 0 : (hidx >= kFastHdrCap ? kFastHdrCap - 1 : hidx);
+                const uint32_t h = T.hdr[hcl];
+                const uint32_t w = gload<uint32_t>(in_pay ? e.srcbase + p : dummy);
+                v[i] = in_pay ? w : h;
+            }
         }
+        store_chunk(a.out, o, lo, min(o + 16, E), v);
     }
 }
 
@@ -338,6 +436,13 @@ hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
     const uint64_t blocks = (num_emit_tiles(a.n) + kTile / 64 - 1) / (kTile / 64);
     hipLaunchKernelGGL(enc_emit_kernel_t<0>, dim3(uint32_t(blocks)), dim3(kTile), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_enc_fixup(const EncArgs& a, hipStream_t s) {
+    uint64_t blocks = (num_emit_tiles(a.n) + kTile / 64 - 1) / (kTile / 64);
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(enc_fixup_kernel, dim3(uint32_t(blocks)), dim3(kTile), 0, s, a);
     return hipGetLastError();
 }
 

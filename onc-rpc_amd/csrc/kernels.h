@@ -23,6 +23,8 @@ struct EncArgs {
     uint32_t* rec_len;      // n, optional
     uint64_t* tile_sum;     // tiles
     const uint64_t* tile_base;  // tiles
+    uint32_t* defer_list;   // tiles: tiles enc_emit left to enc_fixup
+    uint32_t* defer_count;  // zeroed by enc_len
 };
 
 struct DecArgs {
@@ -35,6 +37,7 @@ struct DecArgs {
 // encode.hip
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s);
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s);
+hipError_t launch_enc_fixup(const EncArgs& a, hipStream_t s);
 // scan.hip
 hipError_t launch_scan_tiles(const uint64_t* in, uint64_t* out_excl, uint64_t count, uint64_t base,
                              uint64_t* total_out, hipStream_t s);

@@ -18,8 +18,9 @@ _LIB = None
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libonc_rpc_amd.so")
 
 K_NAMES = ["enc_len_kernel", "scan_tiles_kernel", "enc_emit_kernel", "decode_kernel",
-           "len_tiles_kernel", "len_apply_kernel"]
-K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY = range(6)
+           "len_tiles_kernel", "len_apply_kernel", "enc_fixup_kernel"]
+K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY, K_ENC_FIXUP = range(7)
+K_COUNT = len(K_NAMES)
 
 # every symbol include/onc_rpc.h declares
 EXPORTED = [
@@ -159,11 +160,11 @@ class Codec:
         self._check(self.lib.onc_codec_enable_timing(self.h, 1 if on else 0), "enable_timing")
 
     def kernel_stats(self):
-        ms = (C.c_double * 6)()
-        cnt = (C.c_uint64 * 6)()
+        ms = (C.c_double * K_COUNT)()
+        cnt = (C.c_uint64 * K_COUNT)()
         self._check(self.lib.onc_codec_kernel_stats(self.h, C.cast(ms, C.c_void_p), C.cast(cnt, C.c_void_p)),
                     "kernel_stats")
-        return {K_NAMES[k]: (ms[k], cnt[k]) for k in range(6)}
+        return {K_NAMES[k]: (ms[k], cnt[k]) for k in range(K_COUNT)}
 
     def reset_stats(self):
         self._check(self.lib.onc_codec_reset_stats(self.h), "reset_stats")
