@@ -237,10 +237,12 @@ const char* onc_codec_last_error(const onc_codec* codec);
 const char* onc_status_str(int32_t status);
 int onc_abi_version(void);
 
-/* Per-kernel event timing (for the bench's roofline). When enabled every
- * kernel launch is bracketed by hipEvents on the codec stream; the
- * accumulated device time and launch count per kernel id are returned by
- * onc_codec_kernel_stats after a sync. Ids: see ONC_K_*. */
+/* Per-kernel event timing (for the bench's roofline). `enable` is a bitmask
+ * of kernel ids (1 << ONC_K_*; ONC_TIMING_ALL = every kernel, 0 = off): each
+ * launch of a selected kernel is bracketed by hipEvents on the codec
+ * stream; the accumulated device time and launch count per kernel id are
+ * returned by onc_codec_kernel_stats after a sync. Timing only the kernel
+ * of interest keeps the event overhead off the other launches. */
 #define ONC_K_ENC_LEN     0
 #define ONC_K_SCAN_TILES  1
 #define ONC_K_ENC_EMIT    2
@@ -249,6 +251,7 @@ int onc_abi_version(void);
 #define ONC_K_LEN_APPLY   5
 #define ONC_K_ENC_FIXUP   6
 #define ONC_K_COUNT       7
+#define ONC_TIMING_ALL    (-1)
 int onc_codec_enable_timing(onc_codec* codec, int enable);
 int onc_codec_kernel_stats(onc_codec* codec, double* ms_total /*[ONC_K_COUNT]*/,
                            uint64_t* launches /*[ONC_K_COUNT]*/);

@@ -15,10 +15,10 @@
 struct onc_codec {
     int device = 0;
     hipStream_t stream = nullptr;
-    // [tile_sum | tile_base | defer_list (u32) | defer_count], 3 * scratch_tiles + 2 u64 entries
+    // scratch (u64 words): [tile_sum | tile_base | defer_list (u32) | block_sum | block_base | counters]
     uint64_t* scratch = nullptr;
     uint64_t scratch_tiles = 0;
-    bool timing = false;
+    uint32_t timing = 0;   // bitmask of ONC_K_* ids whose launches are bracketed
     struct Pending {
         int kernel;
         hipEvent_t start, stop;
@@ -54,13 +54,14 @@ hipEvent_t take_event(onc_codec* c) {
 template <class F>
 int run(onc_codec* c, int kernel, const char* what, F&& launch) {
     hipEvent_t a = nullptr, b = nullptr;
-    if (c->timing) {
+    const bool timed = (c->timing >> kernel) & 1u;
+    if (timed) {
         a = take_event(c);
         b = take_event(c);
         if (a) hipEventRecord(a, c->stream);
     }
     const hipError_t e = launch();
-    if (c->timing && a && b) {
+    if (timed && a && b) {
         hipEventRecord(b, c->stream);
         c->pending.push_back({kernel, a, b});
     }
@@ -79,13 +80,25 @@ int ensure_scratch(onc_codec* c, uint64_t tiles) {
         c->scratch = nullptr;
         c->scratch_tiles = 0;
     }
-    hipError_t e = hipMalloc(&c->scratch, (3 * want + 2) * sizeof(uint64_t));
+    hipError_t e = hipMalloc(&c->scratch, (3 * want + 2 * (want / 4 + 1) + 16) * sizeof(uint64_t));
     if (e != hipSuccess) {
         fail(c, e, "hipMalloc(scratch)");
         return ONC_RC_ENOMEM;
     }
     c->scratch_tiles = want;
     return ONC_RC_OK;
+}
+
+// Points the encoder's per-call state into the codec scratch.
+void bind_scratch(onc_codec* c, onc::EncArgs& a) {
+    const uint64_t T = c->scratch_tiles;
+    const uint64_t B = T / 4 + 1;
+    a.tile_sum = c->scratch;
+    a.tile_base = c->scratch + T;
+    a.defer_list = reinterpret_cast<uint32_t*>(c->scratch + 2 * T);
+    a.block_sum = c->scratch + 3 * T;
+    a.block_base = c->scratch + 3 * T + B;
+    a.defer_count = reinterpret_cast<uint32_t*>(c->scratch + 3 * T + 2 * B + 8);
 }
 
 int set_device(onc_codec* c) {
@@ -193,7 +206,7 @@ const char* onc_kernel_name(int k) {
 
 int onc_codec_enable_timing(onc_codec* c, int enable) {
     if (!c) return ONC_RC_EINVAL;
-    c->timing = enable != 0;
+    c->timing = uint32_t(enable) & ((1u << ONC_K_COUNT) - 1u);
     return ONC_RC_OK;
 }
 
@@ -252,8 +265,7 @@ int onc_encode_lengths(onc_codec* c, const onc_batch* batch, uint32_t* rec_len, 
     a.payload_arena = batch->payload_arena;
     a.status = status;
     a.rec_len = rec_len;
-    a.tile_sum = c->scratch;
-    a.defer_count = reinterpret_cast<uint32_t*>(c->scratch + 3 * c->scratch_tiles);
+    bind_scratch(c, a);
     return run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
 }
 
@@ -281,15 +293,15 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
     a.rec_off = rec_off;
     a.status = status;
     a.rec_len = rec_len;
-    a.tile_sum = c->scratch;
-    a.tile_base = c->scratch + c->scratch_tiles;
-    a.defer_list = reinterpret_cast<uint32_t*>(c->scratch + 2 * c->scratch_tiles);
-    a.defer_count = reinterpret_cast<uint32_t*>(c->scratch + 3 * c->scratch_tiles);
+    bind_scratch(c, a);
+    // enc_len: plans + tile/workgroup totals; scan: workgroup bases (and the
+    // grand total into rec_off[n]); enc_emit: bytes; enc_fixup: tiles
+    // enc_emit deferred (exits at once when there are none).
     rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
-    rc = run(c, ONC_K_SCAN_TILES, "scan_tiles", [&] {
-        return onc::launch_scan_tiles(a.tile_sum, c->scratch + c->scratch_tiles, tiles, 0, rec_off + batch->n,
-                                      c->stream);
+    const uint64_t nblk = onc::num_tiles(batch->n);
+    rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
+        return onc::launch_scan_tiles(a.block_sum, a.block_base, nblk, 0, rec_off + batch->n, c->stream);
     });
     if (rc != ONC_RC_OK) return rc;
     rc = run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });

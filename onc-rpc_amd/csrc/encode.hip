@@ -27,9 +27,11 @@
 
 namespace onc {
 
-// Per-record plan + per-tile (kEmitRecs = 64 records = one wavefront)
-// byte totals: the wave's inclusive __shfl scan, lane 63 writes the total.
+// Per-record plan + per-tile byte totals: tile = kEmitRecs (64) records =
+// one wavefront (its inclusive __shfl scan, lane 63 writes the total), and
+// per-workgroup totals (kTile = 256 records = 4 tiles) for the scan.
 __global__ __launch_bounds__(kTile) void enc_len_kernel(EncArgs a) {
+    __shared__ uint64_t s_wave[kTile / 64];
     const uint64_t r = uint64_t(blockIdx.x) * kTile + threadIdx.x;
     uint64_t len = 0;
     if (r < a.n) {
@@ -41,8 +43,13 @@ __global__ __launch_bounds__(kTile) void enc_len_kernel(EncArgs a) {
     }
     const uint64_t incl = wave_incl_scan_u64(len);
     const uint64_t tile = r / kEmitRecs;
-    if ((threadIdx.x & 63) == 63 && tile * kEmitRecs < a.n) a.tile_sum[tile] = incl;
+    if ((threadIdx.x & 63) == 63) {
+        if (tile * kEmitRecs < a.n) a.tile_sum[tile] = incl;
+        s_wave[threadIdx.x >> 6] = incl;
+    }
     if (r == 0) *a.defer_count = 0;   // enc_emit appends to the deferred-tile list
+    __syncthreads();
+    if (threadIdx.x == 0 && a.block_sum) a.block_sum[blockIdx.x] = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
 }
 
 // Largest r in [0, nrec) with start[r] <= x (start ascending). Records of
@@ -338,9 +345,13 @@ __global__ __launch_bounds__(kTile) void enc_emit_kernel_t(EncArgs a) {
     const uint64_t tile = uint64_t(blockIdx.x) * (kTile / 64) + wv;
     const uint64_t r0 = tile * kEmitRecs;
     if (r0 >= a.n) return;
+    // tile base = workgroup base (scan of enc_len's workgroup totals) + the
+    // totals of the tiles before this one in the workgroup
+    uint64_t T0 = a.block_base[blockIdx.x];
+    for (int w = 0; w < wv; ++w) T0 += a.tile_sum[uint64_t(blockIdx.x) * (kTile / 64) + w];
+    if (lane == 0) a.tile_base[tile] = T0;            // read by enc_fixup
     FastTile& T = s_tiles[wv];
     const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
-    const uint64_t T0 = a.tile_base[tile];
     const uintptr_t payload = reinterpret_cast<uintptr_t>(a.payload_arena);
 
     onc_msg d;

@@ -22,9 +22,11 @@ struct EncArgs {
     int32_t* status;        // n
     uint32_t* rec_len;      // n, optional
     uint64_t* tile_sum;     // tiles
-    const uint64_t* tile_base;  // tiles
+    uint64_t* tile_base;    // tiles (written by enc_emit, read by enc_fixup)
     uint32_t* defer_list;   // tiles: tiles enc_emit left to enc_fixup
     uint32_t* defer_count;  // zeroed by enc_len
+    uint64_t* block_sum;    // enc_len workgroups (256 records): byte totals
+    uint64_t* block_base;   // exclusive scan of block_sum
 };
 
 struct DecArgs {
@@ -47,7 +49,7 @@ hipError_t launch_len_apply(const uint32_t* len, uint64_t n, const uint64_t* til
 // decode.hip
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s);
 
-inline uint64_t num_tiles(uint64_t n) { return (n + 255) / 256; }
-inline uint64_t num_emit_tiles(uint64_t n) { return (n + kEmitRecs - 1) / kEmitRecs; }
+__host__ __device__ inline uint64_t num_tiles(uint64_t n) { return (n + 255) / 256; }
+__host__ __device__ inline uint64_t num_emit_tiles(uint64_t n) { return (n + kEmitRecs - 1) / kEmitRecs; }
 
 }  // namespace onc

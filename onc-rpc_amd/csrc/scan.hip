@@ -10,25 +10,38 @@
 
 namespace onc {
 
-// Exclusive scan of `count` u64 tile totals by one 1024-thread workgroup.
-// Each thread owns a contiguous segment; the per-thread sums are combined
-// with the wave/LDS block scan.
+// Exclusive scan of `count` u64 totals by one 1024-thread workgroup. Each
+// thread owns a contiguous segment and reads it in batches of 8 independent
+// loads (one memory latency per batch, not per element); the per-thread
+// sums are combined by the wavefront __shfl + LDS block scan.
 __global__ __launch_bounds__(kScanThreads) void scan_tiles_kernel(const uint64_t* in, uint64_t* out,
                                                                     uint64_t count, uint64_t base,
                                                                     uint64_t* total_out) {
     __shared__ uint64_t s_wave[kScanThreads / 64];
+    constexpr int kB = 8;
     const uint64_t per = (count + kScanThreads - 1) / kScanThreads;
     const uint64_t lo = min(count, uint64_t(threadIdx.x) * per);
     const uint64_t hi = min(count, lo + per);
     uint64_t sum = 0;
-    for (uint64_t j = lo; j < hi; ++j) sum += in[j];
+    for (uint64_t j = lo; j < hi; j += kB) {
+        uint64_t v[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) v[k] = j + k < hi ? in[j + k] : 0;
+#pragma unroll
+        for (int k = 0; k < kB; ++k) sum += v[k];
+    }
     uint64_t total;
     const uint64_t excl = block_excl_scan_u64<kScanThreads>(sum, s_wave, &total);
     uint64_t run = base + excl;
-    for (uint64_t j = lo; j < hi; ++j) {
-        const uint64_t v = in[j];
-        out[j] = run;
-        run += v;
+    for (uint64_t j = lo; j < hi; j += kB) {
+        uint64_t v[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) v[k] = j + k < hi ? in[j + k] : 0;
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            if (j + k < hi) out[j + k] = run;
+            run += v[k];
+        }
     }
     if (threadIdx.x == 0 && total_out) *total_out = base + total;
 }

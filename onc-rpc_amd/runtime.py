@@ -156,8 +156,15 @@ class Codec:
     def reserve(self, n):
         self._check(self.lib.onc_codec_reserve(self.h, n), "onc_codec_reserve")
 
-    def enable_timing(self, on=True):
-        self._check(self.lib.onc_codec_enable_timing(self.h, 1 if on else 0), "enable_timing")
+    def enable_timing(self, on=True, kernels=None):
+        """Bracket launches with HIP events: every kernel (on=True), none
+        (on=False), or only the ids in `kernels` (K_* constants)."""
+        mask = -1 if on else 0
+        if on and kernels is not None:
+            mask = 0
+            for k in kernels:
+                mask |= 1 << k
+        self._check(self.lib.onc_codec_enable_timing(self.h, mask), "enable_timing")
 
     def kernel_stats(self):
         ms = (C.c_double * K_COUNT)()

@@ -228,7 +228,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d_auth, 64));
     CK(hipMalloc(&d_unix, sizeof(onc_unix_params)));
     CK(hipMalloc(&d_off, (n + 1) * 8));
-    CK(hipMalloc(&d_scr, 3 * tiles * 8 + 64));
+    CK(hipMalloc(&d_scr, (3 * tiles + 2 * (tiles / 4 + 1) + 16) * 8));
     CK(hipMalloc(&d_st, n * 4));
     CK(hipMemcpy(d_msgs, msgs.data(), n * sizeof(onc_msg), hipMemcpyHostToDevice));
     CK(hipMemcpy(d_pay, pay.data(), pay.size(), hipMemcpyHostToDevice));
@@ -246,9 +246,11 @@ int main(int argc, char** argv) {
     a.tile_sum = d_scr;
     a.tile_base = d_scr + tiles;
     a.defer_list = reinterpret_cast<uint32_t*>(d_scr + 2 * tiles);
-    a.defer_count = reinterpret_cast<uint32_t*>(d_scr + 3 * tiles);
+    a.block_sum = d_scr + 3 * tiles;
+    a.block_base = d_scr + 3 * tiles + tiles / 4 + 1;
+    a.defer_count = reinterpret_cast<uint32_t*>(d_scr + 3 * tiles + 2 * (tiles / 4 + 1) + 8);
     CK(launch_enc_len(a, 0));
-    CK(launch_scan_tiles(a.tile_sum, d_scr + tiles, tiles, 0, d_off + n, 0));
+    CK(launch_scan_tiles(a.block_sum, a.block_base, num_tiles(n), 0, d_off + n, 0));
     CK(launch_enc_emit(a, 0));
     CK(launch_enc_fixup(a, 0));
     CK(hipDeviceSynchronize());
@@ -267,8 +269,10 @@ int main(int argc, char** argv) {
     a2.out = d_out2;
     const uint64_t n16 = (n * W + 15) / 16;
     std::vector<Var> vars = {
-        {"product_emit", true, [&] { launch_enc_emit(a2, 0); launch_enc_fixup(a2, 0); }},
-        {"product_fixup_all_tiles", false, [&] { hipLaunchKernelGGL(fill_all_tiles, dim3(1), dim3(1), 0, 0, a2.defer_list, a2.defer_count, uint32_t(tiles)); launch_enc_fixup(a2, 0); }},
+        {"product_len_scan_emit_fixup", true, [&] { launch_enc_len(a2, 0); launch_scan_tiles(a2.block_sum, a2.block_base, num_tiles(n), 0, d_off + n, 0); launch_enc_emit(a2, 0); launch_enc_fixup(a2, 0); }},
+        {"product_scan", false, [&] { launch_scan_tiles(a2.block_sum, a2.block_base, num_tiles(n), 0, d_off + n, 0); }},
+        {"product_emit_only", false, [&] { launch_enc_emit(a2, 0); }},
+        
         {"copy_256MB_payload_ideal", false,
          [&] { hipLaunchKernelGGL(v_copy, dim3(2048), dim3(256), 0, 0, (const uint4*)d_pay, (uint4*)d_out2, n * P / 16); }},
         {"fixed_structured_copy", false,
