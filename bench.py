@@ -236,8 +236,8 @@ def main():
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("kernel") == dom and tj.get("records") == n:
-            traffic = tj.get("hbm_bytes_per_launch")
+        if tj.get("records") == n and dom in tj.get("kernels", {}):
+            traffic = tj["kernels"][dom]["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         pass
     roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
