@@ -7,12 +7,21 @@ RpcMessage::serialise_into of every record into one send buffer
 (src/rpc_message.rs:136-164) followed by RpcMessage::try_from of every
 record of that buffer (src/rpc_message.rs:235-271), inputs resident in HBM.
 
-Workload (N=1): configs[1] — 1M Call(prog 100003, vers 4, proc 1,
-AuthNone(None) x2) with a 256 B random payload (W = 300 B on the wire),
-encode -> decode loopback. For --gpus N every rank processes its own 1M
-record shard (weak scaling, no data-path collective).
+Workloads (--workload; the default is the headline line):
+  c1  configs[1] — 1M Call(prog 100003, vers 4, proc 1, AuthNone(None) x2)
+      + 256 B random payload (W = 300 B), encode -> decode loopback.
+  c2  configs[2] — 1M mixed Call/Reply, payloads 64..4096 B: decode step =
+      scan of rec_len into offsets + decode (input wire encoded once, untimed).
+  c3  configs[3] — 4M Call(AuthUnix 16 gids) + 1 KiB payload (W = 1152),
+      encode -> decode loopback.
+For --gpus N every rank processes its own shard of --records records per GPU
+(weak scaling, no data-path collective).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Besides the device-resident `value`, every run also times the PCIe-inclusive
+rate (pinned host inputs -> H2D -> kernels -> D2H of the outputs), reported
+as `pcie_inclusive` (never as `value`).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c2|c3]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
@@ -26,6 +35,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "device-resident ONC-RPC encode+decode: Mmsgs/s and GiB/s vs HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+DEFAULT_RECORDS = {"c1": 1_000_000, "c2": 1_000_000, "c3": 4_000_000}
 
 
 def parse():
@@ -33,11 +43,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--records", type=int, default=1_000_000, help="records per GPU")
-    ap.add_argument("--payload", type=int, default=256)
+    ap.add_argument("--workload", choices=["c1", "c2", "c3"], default="c1")
+    ap.add_argument("--records", type=int, default=None, help="records per GPU")
     ap.add_argument("--mode", choices=["slice", "bytes"], default="slice")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--pcie-reps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return ap.parse_args()
 
@@ -55,39 +68,84 @@ def cpu_info():
     return model, os.cpu_count()
 
 
-def cpu_baseline(hb, gpu_wire_prefix, seconds, mode):
-    """Oracle (C restatement of the reference, single thread) on a bounded
-    sample of the same workload: encode+decode round trips until `seconds`
-    of CPU work. Also checks the sample's bytes against the GPU output."""
+def parsed_bytes(hb, rec_len):
+    """H per record (SURVEY §8 notation): wire bytes minus the payload and
+    minus opaque bodies + padding, which a zero-copy decode returns as slices."""
+    import numpy as np
+    import onc_rpc_amd.layout as L
+    m = hb.msgs
+    h = rec_len.astype(np.int64) - m["payload_len"].astype(np.int64)
+    for f in ("cred", "verf"):
+        kl = m[f + "_kind_len"]
+        kind = kl >> 24
+        ln = (kl & 0xFFFFFF).astype(np.int64)
+        h -= np.where(kind != L.KIND_UNIX, (ln + 3) // 4 * 4, 0)
+        isu = kind == L.KIND_UNIX
+        if isu.any():
+            nl = hb.unix["name_len"][m[f + "_ref"][isu].astype(np.int64)].astype(np.int64)
+            h[isu] -= (nl + 3) // 4 * 4
+    return h
+
+
+def cpu_baseline(args, hb, gpu_wire_prefix, wire_np, rec_off_np, mode):
+    """Oracle (C restatement of the reference) on the GPU box's host cores, on
+    a bounded sample of the same workload: `--cpu-threads` threads over the
+    whole batch (contiguous partition), and 1 thread on a 20k-record slice.
+    Also checks a slice of the CPU output against the GPU's bytes."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
 
     import oracle_ffi
     import onc_rpc_amd.layout as L
 
-    chunk = 20_000
+    model, ncpu = cpu_info()
+    threads = max(1, min(args.cpu_threads, ncpu or 1))
+    decode_only = args.workload == "c2"
+    chunk = min(20_000, hb.n)
     sub = L.HostBatch(hb.msgs[:chunk].copy(), hb.unix, hb.auth_arena, hb.payload_arena)
     wire, off, st, _ = oracle_ffi.encode_batch(sub)
     parity = wire == gpu_wire_prefix[: len(wire)]
-    w = np.frombuffer(wire + b"\0" * 16, np.uint8).copy()
-    done = 0
-    t0 = time.perf_counter()
-    while True:
-        wire, off, st, _ = oracle_ffi.encode_batch(sub)
-        w = np.frombuffer(wire + b"\0" * 16, np.uint8)
-        oracle_ffi.decode_batch(w, off, mode)
-        done += chunk
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    model, ncpu = cpu_info()
+
+    def run(seconds, fn, per):
+        done = 0
+        t0 = time.perf_counter()
+        while True:
+            fn()
+            done += per
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return done, el
+
+    # single thread, 20k-record slices
+    w1 = np.frombuffer(wire + b"\0" * 16, np.uint8)
+
+    def one():
+        if not decode_only:
+            oracle_ffi.encode_batch(sub)
+        oracle_ffi.decode_batch(w1, off, mode)
+    d1, e1 = run(args.cpu_seconds / 2, one, chunk)
+
+    # all threads, whole batch
+    if decode_only:
+        def many():
+            oracle_ffi.decode_batch(wire_np, rec_off_np, mode, threads=threads)
+    else:
+        buf = np.zeros(int(rec_off_np[-1]) + 16, np.uint8)
+
+        def many():
+            out, ro, _, _ = oracle_ffi.encode_batch_mt(hb, threads, out=buf)
+            oracle_ffi.decode_batch(out, ro, mode, threads=threads)
+    dn, en = run(args.cpu_seconds / 2, many, hb.n)
+    what = "decode" if decode_only else "encode+decode round trip"
     return {
-        "value": done / el / 1e6,
+        "value": dn / en / 1e6,
         "unit": "Mmsgs/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"{done} records ({chunk}-record chunks of the same configs[1] workload), "
-                  f"encode+decode round trip, {el:.1f} s on 1 thread of {ncpu}-CPU host ({model})",
+        "sample": f"{dn} records ({hb.n}-record batches of the same {args.workload} workload, {what}) in "
+                  f"{en:.1f} s on {threads} threads (contiguous record partition) of a {ncpu}-CPU host ({model})",
+        "single_thread": {"value": d1 / e1 / 1e6, "unit": "Mmsgs/s", "cores": 1,
+                          "sample": f"{d1} records ({chunk}-record slices) in {e1:.1f} s"},
         "sample_bit_exact_vs_gpu": bool(parity),
     }
 
@@ -109,33 +167,56 @@ def main():
     import onc_rpc_amd.synth as S
 
     dist = None
+    torch.cuda.set_device(local_rank)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     mode = L.DECODE_BYTES if args.mode == "bytes" else L.DECODE_SLICE
+    wl = args.workload
+    per_gpu = args.records or DEFAULT_RECORDS[wl]
 
-    n_total = args.records * world
+    n_total = per_gpu * world
     lo, hi = SH.shard_bounds(n_total, world, rank)
     n = hi - lo
-    W = 4 * 11 + args.payload                 # Call(AuthNone x2): 44 B header + payload
-    H = 44                                    # parsed header bytes per record
-    hb = S.call_none(n, args.payload, seed=1 + rank, first_xid=lo)
+    if wl == "c1":
+        hb = S.call_none(n, 256, seed=1 + rank, first_xid=lo)
+        desc = "configs[1]: Call(prog 100003, vers 4, proc 1, AuthNone(None) x2) + 256 B payload, encode -> decode"
+    elif wl == "c2":
+        hb = S.mixed(n, seed=2 + rank)
+        desc = "configs[2]: mixed Call/Reply (payloads 64..4096 B), rec_len scan + decode"
+    else:
+        hb = S.call_unix16(n, 1024, seed=3 + rank)
+        desc = "configs[3]: Call(AuthUnix 16 gids) + AuthNone + 1 KiB payload, encode -> decode"
     db = R.DeviceBatch.from_host(hb, dev)
     codec = R.Codec(local_rank)
     codec.reserve(n)
 
-    out = torch.empty(n * W + 16, dtype=torch.uint8, device=dev)
+    # record lengths (device), output sized to the exact total
+    rec_len = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    enc_status = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    codec.encode_lengths(db, rec_len, enc_status)
+    lens_np = rec_len[:n].cpu().numpy().view(np.uint32).astype(np.int64)
+    total_bytes = int(lens_np.sum())
+    out = torch.zeros(total_bytes + 16, dtype=torch.uint8, device=dev)
     rec_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    enc_status = torch.empty(n, dtype=torch.int32, device=dev)
+    dec_off = rec_off
     dec = R.DecodeBuffers(n, dev)
+    H = parsed_bytes(hb, lens_np)
+    sum_W, sum_H = total_bytes, int(H.sum())
 
-    def step():
-        codec.encode(db, out, rec_off, enc_status)
-        codec.decode(out, rec_off, n, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1)
+    if wl == "c2":
+        codec.encode(db, out, rec_off, enc_status, rec_len)     # input wire (untimed)
+        torch.cuda.synchronize()
+        dec_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+
+        def step():
+            codec.scan_lengths(rec_len, n, 0, dec_off)
+            codec.decode(out, dec_off, n, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1)
+    else:
+        def step():
+            codec.encode(db, out, rec_off, enc_status)
+            codec.decode(out, rec_off, n, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1)
 
     def barrier():
         if dist is not None:
@@ -195,55 +276,100 @@ def main():
 
     # Validation of the last step (device-side, size-independent checks).
     ok = True
-    if int((enc_status != 0).sum()) or int((dec.status != 0).sum()):
+    if wl != "c2" and int((enc_status[:n] != 0).sum()):
         ok = False
-    if int(rec_off[n]) != n * W:
+    if int((dec.status[:n] != 0).sum()):
+        ok = False
+    if int(dec_off[n]) != total_bytes:
         ok = False
     xid = dec.msgs.view(-1, 64)[:n, 0:4].contiguous().view(torch.int32).view(-1)
-    if not torch.equal(xid, (torch.arange(lo, hi, device=dev, dtype=torch.int64) & 0xFFFFFFFF).to(torch.int32)):
+    want_xid = torch.from_numpy(hb.msgs["xid"].view(np.int32).copy()).to(dev)
+    if not torch.equal(xid, want_xid):
         ok = False
     okt = torch.tensor([1 if ok else 0], device=dev)
     if dist is not None:
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
     ok = bool(okt.item())
 
+    # PCIe-inclusive rate: pinned host inputs -> H2D -> step -> D2H outputs.
+    pcie = None
+    if not args.no_pcie:
+        if wl == "c2":
+            d_in = [out, rec_len]
+            d_out = [dec_off, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1]
+        else:
+            d_in = [db.msgs, db.unix, db.auth_arena, db.payload_arena]
+            d_out = [out, rec_off, enc_status, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1]
+        h_in = [x.cpu().pin_memory() for x in d_in]
+        h_out = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in d_out]
+        bytes_h2d = sum(x.numel() * x.element_size() for x in h_in)
+        bytes_d2h = sum(x.numel() * x.element_size() for x in h_out)
+
+        def pcie_step():
+            for d, h in zip(d_in, h_in):
+                d.copy_(h, non_blocking=True)
+            step()
+            for h, d in zip(h_out, d_out):
+                h.copy_(d, non_blocking=True)
+        pcie_step()
+        torch.cuda.synchronize()
+        barrier()
+        e4 = torch.cuda.Event(enable_timing=True)
+        e5 = torch.cuda.Event(enable_timing=True)
+        e4.record()
+        for _ in range(args.pcie_reps):
+            pcie_step()
+        e5.record()
+        torch.cuda.synchronize()
+        pms = e4.elapsed_time(e5) / args.pcie_reps
+        pt = torch.tensor([pms], dtype=torch.float64, device=dev)
+        if dist is not None:
+            dist.all_reduce(pt, op=dist.ReduceOp.MAX)
+        pms = float(pt[0])
+        pcie = {"value": n_total / (pms / 1e3) / 1e6, "unit": "Mmsgs/s", "ms_per_step": pms,
+                "h2d_bytes_per_gpu": bytes_h2d, "d2h_bytes_per_gpu": bytes_d2h,
+                "pcie_GBs_per_gpu": (bytes_h2d + bytes_d2h) / (pms / 1e3) / 1e9,
+                "note": "pinned host buffers; H2D, kernels and D2H serialized on one stream"}
+
     steps = args.steps
     ms_per_step = ms_max / steps
     value = n_total / (ms_per_step / 1e3) / 1e6       # whole-job Mmsgs/s
-    wire_gibs = n_total * W / (ms_per_step / 1e3) / 2**30
+    wire_gibs = sum_W * world / (ms_per_step / 1e3) / 2**30
 
     # Roofline of the dominant kernel (per-launch averages from HIP events).
-    per_rec_alg = {
-        "enc_len_kernel": 64 + 4 + 4,      # descriptor read + status + rec_len writes
-        "scan_tiles_kernel": 0,            # per-workgroup totals only (~n/16 B)
-        "enc_emit_kernel": 2 * W,          # encode reads ~W, writes W
-        "decode_kernel": 2 * H + 4,        # zero-copy decode
-        "len_tiles_kernel": 4,
-        "len_apply_kernel": 12,
-        "enc_fixup_kernel": 0,             # deferred tiles only (none for this workload)
+    # Algorithmic bytes per launch, SURVEY §8(d): encode reads ~W and writes
+    # W; zero-copy decode reads H + 4 (the length) and writes ~H.
+    alg_bytes = {
+        "enc_len_kernel": n * (64 + 4),          # descriptor read + status write
+        "scan_tiles_kernel": 0,
+        "enc_emit_kernel": 2 * sum_W,
+        "decode_kernel": 2 * sum_H + 4 * n,
+        "len_tiles_kernel": 4 * n,
+        "len_apply_kernel": 12 * n,
+        "enc_fixup_kernel": 0,                   # deferred tiles only
     }
     kern = {}
     for name, (tot_ms, cnt) in breakdown.items():
         if cnt:
             kern[name] = {"avg_us": tot_ms / cnt * 1e3, "launches": cnt,
-                          "alg_bytes_per_launch": per_rec_alg[name] * n}
+                          "alg_bytes_per_launch": alg_bytes[name]}
     dom = R.K_NAMES[dom_id]
     dom_ms, dom_cnt = kstats[dom]
     dom_us = dom_ms / dom_cnt * 1e3
-    alg = per_rec_alg[dom] * n
+    alg = alg_bytes[dom]
     achieved = alg / (dom_us * 1e-6) / 1e9
     traffic = None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("records") == n and dom in tj.get("kernels", {}):
+        if tj.get("records") == n and tj.get("workload_id", "c1") == wl and dom in tj.get("kernels", {}):
             traffic = tj["kernels"][dom]["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         pass
     roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "alg_bytes_per_launch": alg, "avg_launch_us": dom_us, "launches_timed": dom_cnt}
-    step_alg = n * (2 * W + 2 * H + 4)      # SURVEY §8(d) loopback rule (692 B/record)
+    step_alg = (2 * sum_H + 4 * n) + (0 if wl == "c2" else 2 * sum_W)
     result = {
         "metric": METRIC,
         "value": value,
@@ -256,22 +382,25 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded): Call(prog 100003, vers 4, proc 1, AuthNone(None) x2) + 256 B random payload",
-        "config": {"workload": f"configs[1]: {n // 1000}k x Call(AuthNone) {args.payload} B payload per GPU, "
-                               f"encode -> decode ({args.mode} mode) loopback, HBM-resident",
-                   "records_per_gpu": n, "wire_bytes_per_record": W, "decode_mode": args.mode,
+        "data": f"synthetic (seeded): {desc}",
+        "config": {"workload": f"{desc}; {n} records per GPU ({args.mode} mode), HBM-resident",
+                   "records_per_gpu": n, "wire_bytes_per_gpu": sum_W, "parsed_bytes_per_gpu": sum_H,
+                   "decode_mode": args.mode,
                    "parallelism": f"record-sharded x{world} (no collective)"},
         "wire_GiB_per_s": wire_gibs,
         "ms_per_step_without_kernel_events": ms_clean_max / steps,
         "step_alg_GBs": step_alg * world / (ms_per_step / 1e3) / 1e9,
         "roofline": roofline,
         "kernels_breakdown_pass": kern,
+        "pcie_inclusive": pcie,
         "validated": ok,
         "wall_s_timed_region": t_wall,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        prefix = out[: 20_000 * W].cpu().numpy().tobytes()
-        result["cpu_baseline"] = cpu_baseline(hb, prefix, args.cpu_seconds, mode)
+        prefix = out[: min(total_bytes, 20_000 * 4300)].cpu().numpy().tobytes()
+        wire_np = out.cpu().numpy()
+        off_np = dec_off.cpu().numpy().view(np.uint64)
+        result["cpu_baseline"] = cpu_baseline(args, hb, prefix, wire_np, off_np, mode)
     elif rank == 0:
         result["cpu_baseline"] = None
     if rank == 0:

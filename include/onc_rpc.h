@@ -292,6 +292,13 @@ int onc_encode(onc_codec* codec, const onc_batch* batch,
 int onc_decode(onc_codec* codec, const uint8_t* wire, const uint64_t* rec_off,
                uint64_t n, int mode, const onc_decoded* out);
 
+/* expected_message_len (src/rpc_message.rs:343-367) of one host buffer: the
+ * record-marking header's length + 4. Returns ONC_OK, or
+ * ONC_ERR_INCOMPLETE_HEADER (len < 4) / ONC_ERR_FRAGMENTED (last-fragment
+ * bit clear). Host memory, synchronous; the framing helper a caller uses to
+ * cut one message out of a socket buffer. */
+int32_t onc_expected_message_len(const uint8_t* data, uint64_t len, uint32_t* out);
+
 /* Exclusive scan of record lengths into offsets:
  * rec_off[0] = base, rec_off[i+1] = rec_off[i] + rec_len[i]  ([dev]). */
 int onc_scan_lengths(onc_codec* codec, const uint32_t* rec_len, uint64_t n,

@@ -1,0 +1,804 @@
+// onc_rpc.hpp — C++ mirror of the reference crate's types over the C ABI.
+//
+// The reference (domodwyer/onc-rpc v0.3.3) is a Rust crate; the Rust
+// toolchain is not in this image, so its public surface for the hot path is
+// restated here in C++17 with the same names, argument meanings and error
+// behaviour (see INTEGRATION.md for the Rust extern "C" binding):
+//
+//   RpcMessage      src/rpc_message.rs:97-233     new, xid, message, call_body,
+//                                                 reply_body, serialised_len,
+//                                                 serialise_into, serialise,
+//                                                 try_from (slice / Bytes mode)
+//   MessageType     src/rpc_message.rs:22-93      Call | Reply
+//   CallBody        src/call_body.rs:17-166       new, rpc_version, program, ...
+//   AuthFlavor      src/auth/flavor.rs:18-174     AuthNone(Option<T>) | AuthUnix |
+//                                                 AuthShort | Unknown{id, data}
+//   AuthUnixParams  src/auth/unix_params.rs:72-245
+//   ReplyBody / AcceptedReply / AcceptedStatus / RejectedReply / AuthError
+//                   src/reply/*.rs
+//   Error           src/errors.rs:6-97            (thrown as onc_rpc::Error)
+//   expected_message_len  src/rpc_message.rs:343-367
+//
+// Values are generic over byte storage in the reference (`T, P:
+// AsRef<[u8]>`); here they hold non-owning `Bytes` views (pointer + length),
+// exactly like the reference's `&'a [u8]` instantiation: decoded messages
+// borrow the caller's wire buffer, encoded messages borrow the caller's
+// payload and auth bodies.
+//
+// All codec work runs on the GPU through libonc_rpc_amd.so:
+//   BatchEncoder  — the caller's serialise_into loop over many messages,
+//                   one onc_encode launch (plus the H2D/D2H copies).
+//   BatchDecoder  — the caller's try_from loop over many records, one
+//                   onc_decode launch.
+//   RpcMessage::serialise_into / serialised_len / try_from — single-message
+//                   forms, implemented as batches of one (for API parity;
+//                   use the batch classes for throughput).
+// There is no CPU codec in this header: the value classes only describe
+// messages; lengths, bytes and parse results always come from the kernels.
+// The reference's panics (auth data > 200 bytes, machine name > 255 bytes,
+// more than 16 gids) are thrown as std::logic_error where the reference
+// panics (constructors) and reported as ONC_ENC_* statuses by the batch
+// encoder.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <variant>
+#include <vector>
+
+#include "onc_rpc.h"
+
+namespace onc_rpc {
+
+// ----------------------------------------------------------------------------
+// Bytes: a borrowed byte slice (&[u8])
+// ----------------------------------------------------------------------------
+struct Bytes {
+    const uint8_t* ptr = nullptr;
+    size_t len = 0;
+    Bytes() = default;
+    Bytes(const uint8_t* p, size_t n) : ptr(p), len(n) {}
+    Bytes(const std::vector<uint8_t>& v) : ptr(v.data()), len(v.size()) {}  // NOLINT
+    const uint8_t* data() const { return ptr; }
+    size_t size() const { return len; }
+    bool empty() const { return len == 0; }
+    std::vector<uint8_t> to_vec() const { return std::vector<uint8_t>(ptr, ptr + len); }
+    bool operator==(const Bytes& o) const { return len == o.len && (len == 0 || std::memcmp(ptr, o.ptr, len) == 0); }
+    bool operator!=(const Bytes& o) const { return !(*this == o); }
+};
+
+// ----------------------------------------------------------------------------
+// Error — src/errors.rs:6-97 (Display strings follow the #[error] attributes)
+// ----------------------------------------------------------------------------
+class Error : public std::exception {
+public:
+    Error(int32_t code, uint32_t aux0 = 0, uint32_t aux1 = 0) : code_(code), aux0_(aux0), aux1_(aux1) {
+        msg_ = describe(code, aux0, aux1);
+    }
+    int32_t code() const { return code_; }
+    // IncompleteMessage{buffer_len, expected}; the offending value for the
+    // Invalid*(u32) variants.
+    uint32_t buffer_len() const { return aux0_; }
+    uint32_t expected() const { return aux1_; }
+    uint32_t value() const { return aux0_; }
+    const char* what() const noexcept override { return msg_.c_str(); }
+    bool operator==(const Error& o) const { return code_ == o.code_ && aux0_ == o.aux0_ && aux1_ == o.aux1_; }
+
+    static std::string describe(int32_t code, uint32_t a0, uint32_t a1) {
+        switch (code) {
+            case ONC_ERR_INCOMPLETE_MESSAGE:
+                return "incomplete rpc message (got " + std::to_string(a0) + " bytes, expected " +
+                       std::to_string(a1) + ")";
+            case ONC_ERR_INCOMPLETE_HEADER: return "incomplete fragment header";
+            case ONC_ERR_FRAGMENTED: return "RPC message is fragmented";
+            case ONC_ERR_INVALID_MESSAGE_TYPE: return "invalid rpc message type " + std::to_string(a0);
+            case ONC_ERR_INVALID_REPLY_TYPE: return "invalid rpc reply type " + std::to_string(a0);
+            case ONC_ERR_INVALID_REPLY_STATUS: return "invalid rpc reply status " + std::to_string(a0);
+            case ONC_ERR_INVALID_AUTH_DATA: return "invalid rpc auth data";
+            case ONC_ERR_INVALID_AUTH_ERROR: return "invalid rpc auth error status " + std::to_string(a0);
+            case ONC_ERR_INVALID_REJECTED_REPLY_TYPE:
+                return "invalid rpc rejected reply type " + std::to_string(a0);
+            case ONC_ERR_INVALID_LENGTH: return "invalid length in rpc message";
+            case ONC_ERR_INVALID_RPC_VERSION: return "invalid rpc version " + std::to_string(a0);
+            case ONC_ERR_INVALID_MACHINE_NAME: return "invalid machine name";
+            case ONC_ERR_IO_UNEXPECTED_EOF: return "i/o error (UnexpectedEof): failed to fill whole buffer";
+            default: {
+                const char* s = onc_status_str(code);
+                return s ? std::string(s) : "error " + std::to_string(code);
+            }
+        }
+    }
+
+private:
+    int32_t code_;
+    uint32_t aux0_, aux1_;
+    std::string msg_;
+};
+
+// Device/runtime failure (not a reference error): HIP error or bad argument.
+class CodecError : public std::runtime_error {
+public:
+    using std::runtime_error::runtime_error;
+};
+
+// ----------------------------------------------------------------------------
+// AuthUnixParams — src/auth/unix_params.rs:72-245
+// ----------------------------------------------------------------------------
+class AuthUnixParams {
+public:
+    // AuthUnixParams::new (unix_params.rs:142-158): panics on a machine name
+    // longer than 255 bytes (:149) or more than 16 gids (Gids, :47).
+    AuthUnixParams(uint32_t stamp, Bytes machine_name, uint32_t uid, uint32_t gid, std::vector<uint32_t> gids)
+        : stamp_(stamp), machine_name_(machine_name), uid_(uid), gid_(gid), gids_(std::move(gids)) {
+        if (machine_name.len > ONC_MAX_MACHINE_NAME_LEN) throw std::logic_error("machine name longer than 255 bytes");
+        if (gids_.size() > ONC_MAX_GIDS) throw std::logic_error("more than 16 gids");
+    }
+    uint32_t stamp() const { return stamp_; }
+    Bytes machine_name() const { return machine_name_; }
+    std::string machine_name_str() const {
+        return std::string(reinterpret_cast<const char*>(machine_name_.ptr), machine_name_.len);
+    }
+    uint32_t uid() const { return uid_; }
+    uint32_t gid() const { return gid_; }
+    // None (nullopt) when there are no gids (unix_params.rs:210-216).
+    std::optional<std::vector<uint32_t>> gids() const {
+        if (gids_.empty()) return std::nullopt;
+        return gids_;
+    }
+    const std::vector<uint32_t>& gids_vec() const { return gids_; }
+    bool operator==(const AuthUnixParams& o) const {
+        return stamp_ == o.stamp_ && machine_name_ == o.machine_name_ && uid_ == o.uid_ && gid_ == o.gid_ &&
+               gids_ == o.gids_;
+    }
+
+private:
+    uint32_t stamp_;
+    Bytes machine_name_;
+    uint32_t uid_, gid_;
+    std::vector<uint32_t> gids_;
+};
+
+// ----------------------------------------------------------------------------
+// AuthFlavor — src/auth/flavor.rs:18-174
+// ----------------------------------------------------------------------------
+class AuthFlavor {
+public:
+    enum class Kind { AuthNone, AuthUnix, AuthShort, Unknown };
+
+    static AuthFlavor none(std::optional<Bytes> data = std::nullopt) {
+        AuthFlavor a(Kind::AuthNone);
+        a.data_ = data;
+        return a;
+    }
+    static AuthFlavor unix(AuthUnixParams p) {
+        AuthFlavor a(Kind::AuthUnix);
+        a.unix_ = std::move(p);
+        return a;
+    }
+    static AuthFlavor short_(Bytes data) {
+        AuthFlavor a(Kind::AuthShort);
+        a.data_ = data;
+        return a;
+    }
+    static AuthFlavor unknown(uint32_t id, Bytes data) {
+        AuthFlavor a(Kind::Unknown);
+        a.id_ = id;
+        a.data_ = data;
+        return a;
+    }
+
+    Kind kind() const { return kind_; }
+    // Wire discriminant (flavor.rs:132-139).
+    uint32_t id() const {
+        switch (kind_) {
+            case Kind::AuthNone: return ONC_AUTH_NONE;
+            case Kind::AuthUnix: return ONC_AUTH_UNIX;
+            case Kind::AuthShort: return ONC_AUTH_SHORT;
+            default: return id_;
+        }
+    }
+    // AuthNone's optional body / AuthShort / Unknown data.
+    std::optional<Bytes> data() const { return data_; }
+    const AuthUnixParams& unix_params() const {
+        if (!unix_) throw std::logic_error("not AuthUnix");
+        return *unix_;
+    }
+    bool operator==(const AuthFlavor& o) const {
+        if (kind_ != o.kind_ || id() != o.id()) return false;
+        if (kind_ == Kind::AuthUnix) return *unix_ == *o.unix_;
+        if (data_.has_value() != o.data_.has_value()) return false;
+        return !data_ || *data_ == *o.data_;
+    }
+
+private:
+    explicit AuthFlavor(Kind k) : kind_(k) {}
+    Kind kind_;
+    uint32_t id_ = 0;
+    std::optional<Bytes> data_;
+    std::optional<AuthUnixParams> unix_;
+};
+
+// ----------------------------------------------------------------------------
+// CallBody — src/call_body.rs:17-166
+// ----------------------------------------------------------------------------
+class CallBody {
+public:
+    CallBody(uint32_t program, uint32_t program_version, uint32_t procedure, AuthFlavor auth_credentials,
+             AuthFlavor auth_verifier, Bytes payload)
+        : program_(program), program_version_(program_version), procedure_(procedure),
+          cred_(std::move(auth_credentials)), verf_(std::move(auth_verifier)), payload_(payload) {}
+    uint32_t rpc_version() const { return 2; }   // RPC_VERSION call_body.rs:10
+    uint32_t program() const { return program_; }
+    uint32_t program_version() const { return program_version_; }
+    uint32_t procedure() const { return procedure_; }
+    const AuthFlavor& auth_credentials() const { return cred_; }
+    const AuthFlavor& auth_verifier() const { return verf_; }
+    Bytes payload() const { return payload_; }
+    bool operator==(const CallBody& o) const {
+        return program_ == o.program_ && program_version_ == o.program_version_ && procedure_ == o.procedure_ &&
+               cred_ == o.cred_ && verf_ == o.verf_ && payload_ == o.payload_;
+    }
+
+private:
+    uint32_t program_, program_version_, procedure_;
+    AuthFlavor cred_, verf_;
+    Bytes payload_;
+};
+
+// ----------------------------------------------------------------------------
+// Replies — src/reply/*.rs
+// ----------------------------------------------------------------------------
+enum class AuthError : uint32_t {   // rejected_reply.rs:130-173
+    Success = 0,
+    BadCredentials = 1,
+    RejectedCredentials = 2,
+    BadVerifier = 3,
+    RejectedVerifier = 4,
+    TooWeak = 5,
+    InvalidResponseVerifier = 6,
+    Failed = 7,
+};
+
+class RejectedReply {   // rejected_reply.rs:24-95
+public:
+    enum class Kind { RpcVersionMismatch, AuthError };
+    static RejectedReply rpc_version_mismatch(uint32_t low, uint32_t high) {
+        RejectedReply r(Kind::RpcVersionMismatch);
+        r.low_ = low;
+        r.high_ = high;
+        return r;
+    }
+    static RejectedReply auth_error(AuthError e) {
+        RejectedReply r(Kind::AuthError);
+        r.err_ = e;
+        return r;
+    }
+    Kind kind() const { return kind_; }
+    std::pair<uint32_t, uint32_t> mismatch() const { return {low_, high_}; }
+    AuthError auth_error() const { return err_; }
+    bool operator==(const RejectedReply& o) const {
+        return kind_ == o.kind_ && (kind_ == Kind::AuthError ? err_ == o.err_ : (low_ == o.low_ && high_ == o.high_));
+    }
+
+private:
+    explicit RejectedReply(Kind k) : kind_(k) {}
+    Kind kind_;
+    uint32_t low_ = 0, high_ = 0;
+    AuthError err_ = AuthError::Success;
+};
+
+class AcceptedStatus {   // accepted_reply.rs:109-231
+public:
+    enum class Kind { Success, ProgramUnavailable, ProgramMismatch, ProcedureUnavailable, GarbageArgs, SystemError };
+    static AcceptedStatus success(Bytes payload) {
+        AcceptedStatus s(Kind::Success);
+        s.payload_ = payload;
+        return s;
+    }
+    static AcceptedStatus program_mismatch(uint32_t low, uint32_t high) {
+        AcceptedStatus s(Kind::ProgramMismatch);
+        s.low_ = low;
+        s.high_ = high;
+        return s;
+    }
+    static AcceptedStatus of(Kind k) { return AcceptedStatus(k); }
+    Kind kind() const { return kind_; }
+    Bytes payload() const { return payload_; }
+    std::pair<uint32_t, uint32_t> mismatch() const { return {low_, high_}; }
+    bool operator==(const AcceptedStatus& o) const {
+        if (kind_ != o.kind_) return false;
+        if (kind_ == Kind::Success) return payload_ == o.payload_;
+        if (kind_ == Kind::ProgramMismatch) return low_ == o.low_ && high_ == o.high_;
+        return true;
+    }
+
+private:
+    explicit AcceptedStatus(Kind k) : kind_(k) {}
+    Kind kind_;
+    Bytes payload_;
+    uint32_t low_ = 0, high_ = 0;
+};
+
+class AcceptedReply {   // accepted_reply.rs:20-77
+public:
+    AcceptedReply(AuthFlavor auth_verifier, AcceptedStatus status)
+        : verf_(std::move(auth_verifier)), status_(std::move(status)) {}
+    const AuthFlavor& auth_verifier() const { return verf_; }
+    const AcceptedStatus& status() const { return status_; }
+    bool operator==(const AcceptedReply& o) const { return verf_ == o.verf_ && status_ == o.status_; }
+
+private:
+    AuthFlavor verf_;
+    AcceptedStatus status_;
+};
+
+class ReplyBody {   // reply_body.rs:16-73
+public:
+    static ReplyBody accepted(AcceptedReply r) { return ReplyBody(std::move(r)); }
+    static ReplyBody denied(RejectedReply r) { return ReplyBody(std::move(r)); }
+    bool is_accepted() const { return std::holds_alternative<AcceptedReply>(v_); }
+    const AcceptedReply* accepted() const { return std::get_if<AcceptedReply>(&v_); }
+    const RejectedReply* denied() const { return std::get_if<RejectedReply>(&v_); }
+    bool operator==(const ReplyBody& o) const { return v_ == o.v_; }
+
+private:
+    explicit ReplyBody(AcceptedReply r) : v_(std::move(r)) {}
+    explicit ReplyBody(RejectedReply r) : v_(std::move(r)) {}
+    std::variant<AcceptedReply, RejectedReply> v_;
+};
+
+// MessageType — rpc_message.rs:22-32
+class MessageType {
+public:
+    static MessageType call(CallBody c) { return MessageType(std::move(c)); }
+    static MessageType reply(ReplyBody r) { return MessageType(std::move(r)); }
+    const CallBody* call_body() const { return std::get_if<CallBody>(&v_); }
+    const ReplyBody* reply_body() const { return std::get_if<ReplyBody>(&v_); }
+    bool operator==(const MessageType& o) const { return v_ == o.v_; }
+
+private:
+    explicit MessageType(CallBody c) : v_(std::move(c)) {}
+    explicit MessageType(ReplyBody r) : v_(std::move(r)) {}
+    std::variant<CallBody, ReplyBody> v_;
+};
+
+enum class DecodeMode { Slice = ONC_DECODE_SLICE, Bytes = ONC_DECODE_BYTES };
+
+// ----------------------------------------------------------------------------
+// Codec: one onc_codec handle (device + stream + scan scratch)
+// ----------------------------------------------------------------------------
+class Codec {
+public:
+    explicit Codec(int device = 0, hipStream_t stream = nullptr) {
+        if (onc_codec_create(&h_, device, stream) != ONC_RC_OK) throw CodecError("onc_codec_create failed");
+    }
+    ~Codec() {
+        if (h_) onc_codec_destroy(h_);
+    }
+    Codec(const Codec&) = delete;
+    Codec& operator=(const Codec&) = delete;
+    onc_codec* get() const { return h_; }
+    void check(int rc, const char* what) const {
+        if (rc != ONC_RC_OK) throw CodecError(std::string(what) + ": " + onc_codec_last_error(h_));
+    }
+    void sync() const { check(onc_codec_sync(h_), "onc_codec_sync"); }
+
+private:
+    onc_codec* h_ = nullptr;
+};
+
+namespace detail {
+
+inline void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw CodecError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Device buffer (bytes), grown on demand.
+class DevBuf {
+public:
+    DevBuf() = default;
+    ~DevBuf() {
+        if (p_) (void)hipFree(p_);
+    }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    void* ensure(size_t n) {
+        if (n == 0) n = 16;
+        if (n > cap_) {
+            if (p_) hip_check(hipFree(p_), "hipFree");
+            p_ = nullptr;
+            hip_check(hipMalloc(&p_, n), "hipMalloc");
+            cap_ = n;
+        }
+        return p_;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p_); }
+
+private:
+    void* p_ = nullptr;
+    size_t cap_ = 0;
+};
+
+}  // namespace detail
+
+// ----------------------------------------------------------------------------
+// RpcMessage — src/rpc_message.rs:97-233
+// ----------------------------------------------------------------------------
+class RpcMessage {
+public:
+    RpcMessage(uint32_t xid, MessageType message) : xid_(xid), message_(std::move(message)) {}
+    uint32_t xid() const { return xid_; }
+    const MessageType& message() const { return message_; }
+    const CallBody* call_body() const { return message_.call_body(); }
+    const ReplyBody* reply_body() const { return message_.reply_body(); }
+    bool operator==(const RpcMessage& o) const { return xid_ == o.xid_ && message_ == o.message_; }
+
+    // serialised_len (rpc_message.rs:201-204), computed by the encoder's
+    // length kernel. Throws std::logic_error where the reference panics.
+    uint32_t serialised_len(Codec& codec) const;
+    // serialise_into (rpc_message.rs:136-164): appends the record to `buf`.
+    void serialise_into(Codec& codec, std::vector<uint8_t>& buf) const;
+    // serialise (rpc_message.rs:193-197)
+    std::vector<uint8_t> serialise(Codec& codec) const;
+    // TryFrom<&[u8]> (rpc_message.rs:235-271) / TryFrom<Bytes> (:273-314):
+    // `buf` must hold exactly one message; the result borrows `buf`.
+    static RpcMessage try_from(Codec& codec, Bytes buf, DecodeMode mode = DecodeMode::Slice);
+
+    // Encode statuses -> the reference's behaviour: panics for the
+    // construction/assert failures, io::Error for TooLong/WriteZero.
+    static void raise_encode_status(int32_t st) {
+        switch (st) {
+            case ONC_OK: return;
+            case ONC_ENC_AUTH_GT_200: throw std::logic_error("auth associated data longer than 200 bytes");
+            case ONC_ENC_NAME_GT_255: throw std::logic_error("machine name longer than 255 bytes");
+            case ONC_ENC_GIDS_GT_16: throw std::logic_error("more than 16 gids");
+            case ONC_ENC_BAD_DESCRIPTOR: throw std::logic_error("invalid message descriptor");
+            case ONC_ENC_TOO_LONG: throw std::runtime_error("message length exceeds maximum");
+            case ONC_ENC_WRITE_ZERO: throw std::runtime_error("failed to write whole buffer");
+            default: throw std::runtime_error(onc_status_str(st));
+        }
+    }
+
+private:
+    uint32_t xid_;
+    MessageType message_;
+};
+
+// ----------------------------------------------------------------------------
+// BatchEncoder: serialise_into of many messages into one send buffer
+// ----------------------------------------------------------------------------
+class BatchEncoder {
+public:
+    // Describe one message (copies its borrowed bytes into the host arenas).
+    void push(const RpcMessage& m);
+    size_t size() const { return msgs_.size(); }
+    void clear() {
+        msgs_.clear();
+        unix_.clear();
+        auth_.clear();
+        payload_.clear();
+    }
+
+    // Encode every pushed message back to back and APPEND the bytes to `out`
+    // (the reference's serialise_into on a Cursor<Vec<u8>> positioned at the
+    // end). Returns one status per message (ONC_OK or ONC_ENC_*; failing
+    // messages occupy 0 bytes). rec_off, if given, receives n+1 offsets
+    // relative to the start of the appended region.
+    std::vector<int32_t> serialise_into(Codec& codec, std::vector<uint8_t>& out,
+                                        std::vector<uint64_t>* rec_off = nullptr);
+    // serialised_len() of every pushed message (0 for failing ones).
+    std::vector<uint32_t> serialised_lens(Codec& codec, std::vector<int32_t>* status = nullptr);
+
+private:
+    void upload(onc_batch& b);
+    void put_auth(const AuthFlavor& a, onc_auth& d);
+
+    std::vector<onc_msg> msgs_;
+    std::vector<onc_unix_params> unix_;
+    std::vector<uint8_t> auth_, payload_;
+    detail::DevBuf d_msgs_, d_unix_, d_auth_, d_payload_, d_out_, d_off_, d_status_, d_len_;
+};
+
+// Result of decoding one record (Result<RpcMessage<&[u8], &[u8]>, Error>).
+struct Decoded {
+    int32_t status = ONC_OK;
+    uint32_t aux0 = 0, aux1 = 0;
+    std::optional<RpcMessage> message;   // set iff status == ONC_OK
+    bool ok() const { return status == ONC_OK; }
+    Error error() const { return Error(status, aux0, aux1); }
+};
+
+// ----------------------------------------------------------------------------
+// BatchDecoder: try_from of many records (one buffer per record)
+// ----------------------------------------------------------------------------
+class BatchDecoder {
+public:
+    // Decode records wire[off_i, off_i + rec_len[i]) back to back (host
+    // buffer). Decoded messages borrow `wire` (zero-copy, like the
+    // reference's &[u8] instantiation), so it must outlive the results.
+    std::vector<Decoded> try_from(Codec& codec, const uint8_t* wire, size_t wire_len,
+                                  const std::vector<uint32_t>& rec_len, DecodeMode mode = DecodeMode::Slice);
+
+private:
+    detail::DevBuf d_wire_, d_len_, d_off_, d_msgs_, d_unix_, d_status_, d_aux0_, d_aux1_;
+};
+
+// expected_message_len (rpc_message.rs:343-367); throws Error.
+inline uint32_t expected_message_len(Bytes data) {
+    uint32_t n = 0;
+    const int32_t st = onc_expected_message_len(data.ptr, data.len, &n);
+    if (st != ONC_OK) throw Error(st);
+    return n;
+}
+
+// ----------------------------------------------------------------------------
+// BatchEncoder implementation
+// ----------------------------------------------------------------------------
+inline void BatchEncoder::put_auth(const AuthFlavor& a, onc_auth& d) {
+    d.id = a.id();
+    switch (a.kind()) {
+        case AuthFlavor::Kind::AuthUnix: {
+            const AuthUnixParams& p = a.unix_params();
+            onc_unix_params u{};
+            u.stamp = p.stamp();
+            u.uid = p.uid();
+            u.gid = p.gid();
+            u.ngids = uint32_t(p.gids_vec().size());
+            for (size_t i = 0; i < p.gids_vec().size(); ++i) u.gids[i] = p.gids_vec()[i];
+            u.name_off = auth_.size();
+            u.name_len = uint32_t(p.machine_name().len);
+            auth_.insert(auth_.end(), p.machine_name().ptr, p.machine_name().ptr + p.machine_name().len);
+            d.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
+            d.ref = unix_.size();
+            unix_.push_back(u);
+            return;
+        }
+        case AuthFlavor::Kind::AuthNone:
+        case AuthFlavor::Kind::AuthShort:
+        case AuthFlavor::Kind::Unknown: {
+            const uint32_t kind = a.kind() == AuthFlavor::Kind::AuthNone    ? ONC_KIND_NONE
+                                  : a.kind() == AuthFlavor::Kind::AuthShort ? ONC_KIND_SHORT
+                                                                            : ONC_KIND_UNKNOWN;
+            const Bytes b = a.data().value_or(Bytes());
+            // Bodies longer than the 24-bit descriptor field cannot be
+            // described; the reference would panic on them (> 200 bytes).
+            if (b.len > 0xFFFFFFu) throw std::logic_error("auth associated data longer than 200 bytes");
+            d.kind_len = ONC_AUTH_PACK(kind, b.len);
+            d.ref = auth_.size();
+            auth_.insert(auth_.end(), b.ptr, b.ptr + b.len);
+            return;
+        }
+    }
+}
+
+inline void BatchEncoder::push(const RpcMessage& m) {
+    onc_msg d{};
+    d.xid = m.xid();
+    if (const CallBody* c = m.call_body()) {
+        d.msg_type = ONC_MSG_CALL;
+        d.u.call.program = c->program();
+        d.u.call.program_version = c->program_version();
+        d.u.call.procedure = c->procedure();
+        put_auth(c->auth_credentials(), d.cred);
+        put_auth(c->auth_verifier(), d.verf);
+        d.payload_len = uint32_t(c->payload().len);
+        d.payload_off = payload_.size();
+        if (c->payload().len > 0xFFFFFFFFull) throw std::runtime_error("message length exceeds maximum");
+        payload_.insert(payload_.end(), c->payload().ptr, c->payload().ptr + c->payload().len);
+    } else {
+        const ReplyBody* r = m.reply_body();
+        d.msg_type = ONC_MSG_REPLY;
+        if (const AcceptedReply* a = r->accepted()) {
+            d.reply_stat = ONC_REPLY_ACCEPTED;
+            put_auth(a->auth_verifier(), d.verf);
+            d.stat = uint8_t(a->status().kind());
+            if (a->status().kind() == AcceptedStatus::Kind::Success) {
+                d.payload_len = uint32_t(a->status().payload().len);
+                d.payload_off = payload_.size();
+                payload_.insert(payload_.end(), a->status().payload().ptr,
+                                a->status().payload().ptr + a->status().payload().len);
+            } else if (a->status().kind() == AcceptedStatus::Kind::ProgramMismatch) {
+                d.u.mismatch.low = a->status().mismatch().first;
+                d.u.mismatch.high = a->status().mismatch().second;
+            }
+        } else {
+            const RejectedReply* j = r->denied();
+            d.reply_stat = ONC_REPLY_DENIED;
+            if (j->kind() == RejectedReply::Kind::RpcVersionMismatch) {
+                d.stat = ONC_REJECT_RPC_MISMATCH;
+                d.u.mismatch.low = j->mismatch().first;
+                d.u.mismatch.high = j->mismatch().second;
+            } else {
+                d.stat = ONC_REJECT_AUTH_ERROR;
+                d.auth_stat = uint8_t(j->auth_error());
+            }
+        }
+    }
+    msgs_.push_back(d);
+}
+
+inline void BatchEncoder::upload(onc_batch& b) {
+    using detail::hip_check;
+    const size_t n = msgs_.size();
+    b.n = n;
+    b.msgs = static_cast<const onc_msg*>(d_msgs_.ensure(n * sizeof(onc_msg)));
+    b.unix_params = static_cast<const onc_unix_params*>(d_unix_.ensure(unix_.size() * sizeof(onc_unix_params)));
+    b.auth_arena = static_cast<const uint8_t*>(d_auth_.ensure(auth_.size() + 16));
+    b.payload_arena = static_cast<const uint8_t*>(d_payload_.ensure(payload_.size() + 16));
+    if (n) hip_check(hipMemcpy(d_msgs_.as<void>(), msgs_.data(), n * sizeof(onc_msg), hipMemcpyHostToDevice), "H2D");
+    if (!unix_.empty())
+        hip_check(hipMemcpy(d_unix_.as<void>(), unix_.data(), unix_.size() * sizeof(onc_unix_params),
+                            hipMemcpyHostToDevice), "H2D");
+    if (!auth_.empty())
+        hip_check(hipMemcpy(d_auth_.as<void>(), auth_.data(), auth_.size(), hipMemcpyHostToDevice), "H2D");
+    if (!payload_.empty())
+        hip_check(hipMemcpy(d_payload_.as<void>(), payload_.data(), payload_.size(), hipMemcpyHostToDevice), "H2D");
+}
+
+inline std::vector<uint32_t> BatchEncoder::serialised_lens(Codec& codec, std::vector<int32_t>* status) {
+    const size_t n = msgs_.size();
+    std::vector<uint32_t> lens(n);
+    std::vector<int32_t> st(n);
+    if (n) {
+        onc_batch b{};
+        upload(b);
+        uint32_t* dl = static_cast<uint32_t*>(d_len_.ensure(n * 4));
+        int32_t* ds = static_cast<int32_t*>(d_status_.ensure(n * 4));
+        codec.check(onc_encode_lengths(codec.get(), &b, dl, ds), "onc_encode_lengths");
+        codec.sync();
+        detail::hip_check(hipMemcpy(lens.data(), dl, n * 4, hipMemcpyDeviceToHost), "D2H");
+        detail::hip_check(hipMemcpy(st.data(), ds, n * 4, hipMemcpyDeviceToHost), "D2H");
+    }
+    if (status) *status = std::move(st);
+    return lens;
+}
+
+inline std::vector<int32_t> BatchEncoder::serialise_into(Codec& codec, std::vector<uint8_t>& out,
+                                                         std::vector<uint64_t>* rec_off) {
+    const size_t n = msgs_.size();
+    std::vector<int32_t> st(n);
+    std::vector<uint64_t> off(n + 1, 0);
+    if (n) {
+        // Size pass (lengths kernel), then the encode into an exact buffer.
+        const std::vector<uint32_t> lens = serialised_lens(codec);
+        uint64_t total = 0;
+        for (uint32_t l : lens) total += l;
+        onc_batch b{};
+        upload(b);
+        uint8_t* dout = static_cast<uint8_t*>(d_out_.ensure(total + 16));
+        uint64_t* doff = static_cast<uint64_t*>(d_off_.ensure((n + 1) * 8));
+        int32_t* ds = static_cast<int32_t*>(d_status_.ensure(n * 4));
+        codec.check(onc_encode(codec.get(), &b, dout, total, doff, ds, nullptr), "onc_encode");
+        codec.sync();
+        const size_t base = out.size();
+        out.resize(base + total);
+        if (total) detail::hip_check(hipMemcpy(out.data() + base, dout, total, hipMemcpyDeviceToHost), "D2H");
+        detail::hip_check(hipMemcpy(st.data(), ds, n * 4, hipMemcpyDeviceToHost), "D2H");
+        detail::hip_check(hipMemcpy(off.data(), doff, (n + 1) * 8, hipMemcpyDeviceToHost), "D2H");
+    }
+    if (rec_off) *rec_off = std::move(off);
+    return st;
+}
+
+// ----------------------------------------------------------------------------
+// BatchDecoder implementation: descriptors -> RpcMessage views over `wire`
+// ----------------------------------------------------------------------------
+namespace detail {
+
+inline AuthFlavor auth_view(const onc_auth& a, const onc_unix_params* unix, const uint8_t* wire) {
+    const uint32_t kind = ONC_AUTH_KIND(a);
+    const uint32_t len = ONC_AUTH_LEN(a);
+    switch (kind) {
+        case ONC_KIND_NONE:
+            // AuthNone with an empty body decodes to None (flavor.rs:71-78)
+            return len == 0 ? AuthFlavor::none() : AuthFlavor::none(Bytes(wire + a.ref, len));
+        case ONC_KIND_UNIX: {
+            const onc_unix_params& u = unix[a.ref];
+            return AuthFlavor::unix(AuthUnixParams(u.stamp, Bytes(wire + u.name_off, u.name_len), u.uid, u.gid,
+                                                   std::vector<uint32_t>(u.gids, u.gids + u.ngids)));
+        }
+        case ONC_KIND_SHORT: return AuthFlavor::short_(Bytes(wire + a.ref, len));
+        default: return AuthFlavor::unknown(a.id, Bytes(wire + a.ref, len));
+    }
+}
+
+inline RpcMessage message_view(const onc_msg& d, const onc_unix_params* unix, const uint8_t* wire) {
+    if (d.msg_type == ONC_MSG_CALL) {
+        return RpcMessage(d.xid, MessageType::call(CallBody(d.u.call.program, d.u.call.program_version,
+                                                            d.u.call.procedure, auth_view(d.cred, unix, wire),
+                                                            auth_view(d.verf, unix, wire),
+                                                            Bytes(wire + d.payload_off, d.payload_len))));
+    }
+    if (d.reply_stat == ONC_REPLY_ACCEPTED) {
+        AcceptedStatus s = AcceptedStatus::of(AcceptedStatus::Kind(d.stat));
+        if (d.stat == ONC_ACCEPT_SUCCESS) s = AcceptedStatus::success(Bytes(wire + d.payload_off, d.payload_len));
+        if (d.stat == ONC_ACCEPT_PROG_MISMATCH) s = AcceptedStatus::program_mismatch(d.u.mismatch.low, d.u.mismatch.high);
+        return RpcMessage(d.xid, MessageType::reply(ReplyBody::accepted(
+                                     AcceptedReply(auth_view(d.verf, unix, wire), std::move(s)))));
+    }
+    RejectedReply j = d.stat == ONC_REJECT_RPC_MISMATCH
+                          ? RejectedReply::rpc_version_mismatch(d.u.mismatch.low, d.u.mismatch.high)
+                          : RejectedReply::auth_error(AuthError(d.auth_stat));
+    return RpcMessage(d.xid, MessageType::reply(ReplyBody::denied(j)));
+}
+
+}  // namespace detail
+
+inline std::vector<Decoded> BatchDecoder::try_from(Codec& codec, const uint8_t* wire, size_t wire_len,
+                                                   const std::vector<uint32_t>& rec_len, DecodeMode mode) {
+    using detail::hip_check;
+    const size_t n = rec_len.size();
+    std::vector<Decoded> res(n);
+    if (!n) return res;
+    uint8_t* dw = static_cast<uint8_t*>(d_wire_.ensure(wire_len + 16));
+    if (wire_len) hip_check(hipMemcpy(dw, wire, wire_len, hipMemcpyHostToDevice), "H2D");
+    uint32_t* dl = static_cast<uint32_t*>(d_len_.ensure(n * 4));
+    hip_check(hipMemcpy(dl, rec_len.data(), n * 4, hipMemcpyHostToDevice), "H2D");
+    uint64_t* doff = static_cast<uint64_t*>(d_off_.ensure((n + 1) * 8));
+    codec.check(onc_scan_lengths(codec.get(), dl, n, 0, doff), "onc_scan_lengths");
+    onc_decoded out{};
+    out.msgs = static_cast<onc_msg*>(d_msgs_.ensure(n * sizeof(onc_msg)));
+    out.unix_params = static_cast<onc_unix_params*>(d_unix_.ensure(2 * n * sizeof(onc_unix_params)));
+    out.status = static_cast<int32_t*>(d_status_.ensure(n * 4));
+    out.aux0 = static_cast<uint32_t*>(d_aux0_.ensure(n * 4));
+    out.aux1 = static_cast<uint32_t*>(d_aux1_.ensure(n * 4));
+    codec.check(onc_decode(codec.get(), dw, doff, n, int(mode), &out), "onc_decode");
+    codec.sync();
+    std::vector<onc_msg> msgs(n);
+    std::vector<onc_unix_params> unix(2 * n);
+    std::vector<int32_t> st(n);
+    std::vector<uint32_t> a0(n), a1(n);
+    hip_check(hipMemcpy(msgs.data(), out.msgs, n * sizeof(onc_msg), hipMemcpyDeviceToHost), "D2H");
+    hip_check(hipMemcpy(unix.data(), out.unix_params, 2 * n * sizeof(onc_unix_params), hipMemcpyDeviceToHost), "D2H");
+    hip_check(hipMemcpy(st.data(), out.status, n * 4, hipMemcpyDeviceToHost), "D2H");
+    hip_check(hipMemcpy(a0.data(), out.aux0, n * 4, hipMemcpyDeviceToHost), "D2H");
+    hip_check(hipMemcpy(a1.data(), out.aux1, n * 4, hipMemcpyDeviceToHost), "D2H");
+    for (size_t i = 0; i < n; ++i) {
+        res[i].status = st[i];
+        res[i].aux0 = a0[i];
+        res[i].aux1 = a1[i];
+        if (st[i] == ONC_OK) res[i].message = detail::message_view(msgs[i], unix.data(), wire);
+    }
+    return res;
+}
+
+// ----------------------------------------------------------------------------
+// RpcMessage single-message forms (batches of one)
+// ----------------------------------------------------------------------------
+inline uint32_t RpcMessage::serialised_len(Codec& codec) const {
+    BatchEncoder e;
+    e.push(*this);
+    std::vector<int32_t> st;
+    const uint32_t n = e.serialised_lens(codec, &st)[0];
+    raise_encode_status(st[0]);
+    return n;
+}
+
+inline void RpcMessage::serialise_into(Codec& codec, std::vector<uint8_t>& buf) const {
+    BatchEncoder e;
+    e.push(*this);
+    raise_encode_status(e.serialise_into(codec, buf)[0]);
+}
+
+inline std::vector<uint8_t> RpcMessage::serialise(Codec& codec) const {
+    std::vector<uint8_t> v;
+    serialise_into(codec, v);
+    return v;
+}
+
+inline RpcMessage RpcMessage::try_from(Codec& codec, Bytes buf, DecodeMode mode) {
+    BatchDecoder d;
+    std::vector<Decoded> r = d.try_from(codec, buf.ptr, buf.len, {uint32_t(buf.len)}, mode);
+    if (!r[0].ok()) throw r[0].error();
+    return std::move(*r[0].message);
+}
+
+}  // namespace onc_rpc

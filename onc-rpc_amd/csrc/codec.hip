@@ -15,7 +15,7 @@
 struct onc_codec {
     int device = 0;
     hipStream_t stream = nullptr;
-    // scratch (u64 words): [tile_sum | tile_base | defer_list (u32) | block_sum | block_base | counters]
+    // scratch (u64 words): [tile_sum | tile_base | block_sum | block_base]
     uint64_t* scratch = nullptr;
     uint64_t scratch_tiles = 0;
     uint32_t timing = 0;   // bitmask of ONC_K_* ids whose launches are bracketed
@@ -58,11 +58,11 @@ int run(onc_codec* c, int kernel, const char* what, F&& launch) {
     if (timed) {
         a = take_event(c);
         b = take_event(c);
-        if (a) hipEventRecord(a, c->stream);
+        if (a) (void)hipEventRecord(a, c->stream);
     }
     const hipError_t e = launch();
     if (timed && a && b) {
-        hipEventRecord(b, c->stream);
+        (void)hipEventRecord(b, c->stream);
         c->pending.push_back({kernel, a, b});
     }
     if (e != hipSuccess) return fail(c, e, what);
@@ -75,8 +75,8 @@ int ensure_scratch(onc_codec* c, uint64_t tiles) {
     while (want < tiles) want *= 2;
     if (c->scratch) {
         // The stream may still be using the old scratch.
-        hipStreamSynchronize(c->stream);
-        hipFree(c->scratch);
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(c->scratch);
         c->scratch = nullptr;
         c->scratch_tiles = 0;
     }
@@ -95,10 +95,9 @@ void bind_scratch(onc_codec* c, onc::EncArgs& a) {
     const uint64_t B = T / 4 + 1;
     a.tile_sum = c->scratch;
     a.tile_base = c->scratch + T;
-    a.defer_list = reinterpret_cast<uint32_t*>(c->scratch + 2 * T);
     a.block_sum = c->scratch + 3 * T;
     a.block_base = c->scratch + 3 * T + B;
-    a.defer_count = reinterpret_cast<uint32_t*>(c->scratch + 3 * T + 2 * B + 8);
+
 }
 
 int set_device(onc_codec* c) {
@@ -131,14 +130,14 @@ int onc_codec_create(onc_codec** out, int device, void* hip_stream) {
 
 int onc_codec_destroy(onc_codec* c) {
     if (!c) return ONC_RC_EINVAL;
-    hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
     for (auto& p : c->pending) {
-        hipEventDestroy(p.start);
-        hipEventDestroy(p.stop);
+        (void)hipEventDestroy(p.start);
+        (void)hipEventDestroy(p.stop);
     }
-    for (auto e : c->spare) hipEventDestroy(e);
-    if (c->scratch) hipFree(c->scratch);
+    for (auto e : c->spare) (void)hipEventDestroy(e);
+    if (c->scratch) (void)hipFree(c->scratch);
     delete c;
     return ONC_RC_OK;
 }
@@ -345,5 +344,16 @@ int onc_scan_lengths(onc_codec* c, const uint32_t* rec_len, uint64_t n, uint64_t
     return run(c, ONC_K_LEN_APPLY, "len_apply",
                [&] { return onc::launch_len_apply(rec_len, n, tile_base, rec_off, c->stream); });
 }
+
+int32_t onc_expected_message_len(const uint8_t* data, uint64_t len, uint32_t* out) {
+    if (out) *out = 0;
+    if (!data || len < 4) return ONC_ERR_INCOMPLETE_HEADER;          // rpc_message.rs:344-346
+    const uint32_t header = (uint32_t(data[0]) << 24) | (uint32_t(data[1]) << 16) |
+                            (uint32_t(data[2]) << 8) | uint32_t(data[3]);
+    if ((header & 0x80000000u) == 0) return ONC_ERR_FRAGMENTED;       // :359-362
+    if (out) *out = (header & 0x7FFFFFFFu) + 4;                       // :365
+    return ONC_OK;
+}
+
 
 }  // extern "C"

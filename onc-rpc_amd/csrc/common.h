@@ -262,62 +262,89 @@ __device__ __forceinline__ uint32_t record_word(const onc_msg& d, uint32_t len, 
 
 // Sequential serialiser of the header words of one planned record (the
 // serialise_into call chain in write order), used to stage headers in LDS.
-// Writes meta_hw(meta) words to dst[0..hw).
-__device__ __forceinline__ uint32_t put_auth_words(const onc_auth& a, const EncSrc& s, uint32_t* dst, uint32_t k) {
+// Emits meta_hw(meta) words, in order, into a sink.
+
+// Sink: plain word stream.
+struct WordSink {
+    uint32_t* dst;
+    __device__ __forceinline__ void operator()(uint32_t w) { *dst++ = w; }
+};
+
+// Sink: the same stream re-aligned to output dwords for a record starting at
+// byte offset m = start & 3 (m != 0): output dword j = stream bytes
+// [4j - m, 4j - m + 4), with bytes outside the header zero. Writes hw + 1
+// words (finish() writes the last one).
+struct ShiftSink {
+    uint32_t* dst;
+    uint32_t prev;
+    uint32_t sh;       // 4 - m
+    __device__ __forceinline__ void operator()(uint32_t w) {
+        *dst++ = funnel(prev, w, sh);
+        prev = w;
+    }
+    __device__ __forceinline__ void finish() { *dst = funnel(prev, 0u, sh); }
+};
+
+template <class Sink>
+__device__ __forceinline__ void put_auth_words(const onc_auth& a, const EncSrc& s, Sink& out) {
     const uint32_t kind = a.kind_len >> 24;
-    dst[k++] = bswap(kind == ONC_KIND_UNKNOWN ? a.id : kind);
+    out(bswap(kind == ONC_KIND_UNKNOWN ? a.id : kind));
     if (kind != ONC_KIND_UNIX) {
         const uint32_t len = a.kind_len & 0xFFFFFFu;
-        dst[k++] = bswap(len);
+        out(bswap(len));
         const uintptr_t b = s.auth_arena + a.ref;
-        for (uint32_t j = 0; 4 * j < len; ++j) dst[k++] = load4_masked(b + 4ull * j, b + len);
-        return k;
+        for (uint32_t j = 0; 4 * j < len; ++j) out(load4_masked(b + 4ull * j, b + len));
+        return;
     }
     const onc_unix_params* u = s.unix + a.ref;
     const uint32_t nl = u->name_len, ng = u->ngids;
-    dst[k++] = bswap(20u + 4u * words4(nl) + 4u * ng);
-    dst[k++] = bswap(u->stamp);
-    dst[k++] = bswap(nl);
+    out(bswap(20u + 4u * words4(nl) + 4u * ng));
+    out(bswap(u->stamp));
+    out(bswap(nl));
     const uintptr_t b = s.auth_arena + u->name_off;
-    for (uint32_t j = 0; 4 * j < nl; ++j) dst[k++] = load4_masked(b + 4ull * j, b + nl);
-    dst[k++] = bswap(u->uid);
-    dst[k++] = bswap(u->gid);
-    dst[k++] = bswap(ng);
-    for (uint32_t j = 0; j < ng; ++j) dst[k++] = bswap(u->gids[j]);
-    return k;
+    for (uint32_t j = 0; 4 * j < nl; ++j) out(load4_masked(b + 4ull * j, b + nl));
+    out(bswap(u->uid));
+    out(bswap(u->gid));
+    out(bswap(ng));
+    for (uint32_t j = 0; j < ng; ++j) out(bswap(u->gids[j]));
 }
 
-__device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, uint32_t* dst) {
-    uint32_t k = 0;
-    dst[k++] = bswap((len - 4u) | 0x80000000u);
-    dst[k++] = bswap(d.xid);
-    dst[k++] = bswap(uint32_t(d.msg_type));
+template <class Sink>
+__device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, Sink& out) {
+    out(bswap((len - 4u) | 0x80000000u));        // record mark, rpc_message.rs:156
+    out(bswap(d.xid));
+    out(bswap(uint32_t(d.msg_type)));
     if (d.msg_type == ONC_MSG_CALL) {
-        dst[k++] = bswap(2u);
-        dst[k++] = bswap(d.u.call.program);
-        dst[k++] = bswap(d.u.call.program_version);
-        dst[k++] = bswap(d.u.call.procedure);
-        k = put_auth_words(d.cred, s, dst, k);
-        put_auth_words(d.verf, s, dst, k);
+        out(bswap(2u));                           // RPC_VERSION call_body.rs:10
+        out(bswap(d.u.call.program));
+        out(bswap(d.u.call.program_version));
+        out(bswap(d.u.call.procedure));
+        put_auth_words(d.cred, s, out);
+        put_auth_words(d.verf, s, out);
         return;
     }
-    dst[k++] = bswap(uint32_t(d.reply_stat));
+    out(bswap(uint32_t(d.reply_stat)));
     if (d.reply_stat == ONC_REPLY_ACCEPTED) {
-        k = put_auth_words(d.verf, s, dst, k);
-        dst[k++] = bswap(uint32_t(d.stat));
+        put_auth_words(d.verf, s, out);
+        out(bswap(uint32_t(d.stat)));
         if (d.stat == ONC_ACCEPT_PROG_MISMATCH) {
-            dst[k++] = bswap(d.u.mismatch.low);
-            dst[k++] = bswap(d.u.mismatch.high);
+            out(bswap(d.u.mismatch.low));
+            out(bswap(d.u.mismatch.high));
         }
         return;
     }
-    dst[k++] = bswap(uint32_t(d.stat));
+    out(bswap(uint32_t(d.stat)));
     if (d.stat == ONC_REJECT_RPC_MISMATCH) {
-        dst[k++] = bswap(d.u.mismatch.low);
-        dst[k++] = bswap(d.u.mismatch.high);
+        out(bswap(d.u.mismatch.low));
+        out(bswap(d.u.mismatch.high));
     } else {
-        dst[k++] = bswap(uint32_t(d.auth_stat));
+        out(bswap(uint32_t(d.auth_stat)));
     }
+}
+
+__device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, uint32_t* dst) {
+    WordSink w{dst};
+    put_header_words(d, len, s, w);
 }
 
 // ---------------------------------------------------------------------------

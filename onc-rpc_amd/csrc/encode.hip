@@ -4,28 +4,29 @@
 // serialise_into/serialised_len chain it calls (call_body.rs:98-119,
 // auth/flavor.rs:106-174, auth/unix_params.rs:162-245, opaque.rs:38-63,
 // reply/*). The reference is called once per message by the user's loop;
-// here one launch encodes a whole batch into one contiguous send buffer.
+// here one pass encodes a whole batch into one contiguous send buffer.
 //
-// Pipeline (3 launches on one stream):
-//   enc_len   lane per record: plan_record() = serialised_len + validation,
-//             per-tile (256-record) byte totals.
-//   scan      exclusive scan of tile totals -> tile base offsets.
-//   enc_emit  per tile: block scan of record lengths (wavefront __shfl scan
-//             + LDS across the 4 waves) -> record offsets; descriptors
-//             staged in LDS; then the tile's output byte range is produced
-//             in 16-byte aligned chunks, one chunk per lane per step, and
-//             stored with global_store_dwordx4 (fully coalesced: a wave
-//             writes 1 KiB contiguous per instruction). Each chunk finds its
-//             record by binary search over the LDS offsets; pure-payload
-//             chunks are an unaligned 16-byte copy (5 dword loads + 4
-//             v_alignbyte); chunks touching header words or a record
-//             boundary evaluate the XDR words directly (record_word()).
-//             Chunks that straddle a tile boundary are written with byte
-//             stores of only this tile's bytes, so tiles never exchange data.
+// Pipeline (4 launches on one stream):
+//   enc_len    lane per record: plan_record() = serialised_len + validation;
+//              per-64-record-tile and per-256-record-workgroup byte totals.
+//   scan       single-workgroup exclusive scan of the workgroup totals.
+//   enc_emit   wave per 64-record tile: wavefront __shfl scan places the
+//              records; headers staged in LDS; the tile's output bytes are
+//              produced in 16-byte chunks, 1 KiB contiguous per wave per step
+//              (global_store_dwordx4). Handles tiles whose records are all
+//              4-byte aligned (every output dword is wholly header or wholly
+//              payload) and whose headers fit LDS; flags the others.
+//   enc_fixup  wave per flagged tile (exits at once for the others): the
+//              byte-general path — header image pre-shifted to each
+//              record's output alignment, payload bytes via clamped dword
+//              loads + v_alignbyte, records in sub-tiles when the headers
+//              exceed LDS.
 #include "common.h"
 #include "kernels.h"
 
 namespace onc {
+
+constexpr uint64_t kDeferBit = 1ull << 63;   // tile_base flag: tile left to enc_fixup
 
 // Per-record plan + per-tile byte totals: tile = kEmitRecs (64) records =
 // one wavefront (its inclusive __shfl scan, lane 63 writes the total), and
@@ -47,51 +48,9 @@ __global__ __launch_bounds__(kTile) void enc_len_kernel(EncArgs a) {
         if (tile * kEmitRecs < a.n) a.tile_sum[tile] = incl;
         s_wave[threadIdx.x >> 6] = incl;
     }
-    if (r == 0) *a.defer_count = 0;   // enc_emit appends to the deferred-tile list
     __syncthreads();
-    if (threadIdx.x == 0 && a.block_sum) a.block_sum[blockIdx.x] = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    if (threadIdx.x == 0) a.block_sum[blockIdx.x] = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
 }
-
-// Largest r in [0, nrec) with start[r] <= x (start ascending). Records of
-// length 0 share their successor's start and are never chosen for an x
-// inside the tile.
-__device__ __forceinline__ int find_rec(const uint64_t* start, int nrec, uint64_t x) {
-    int lo = 0, hi = nrec - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (start[mid] <= x) lo = mid;
-        else hi = mid - 1;
-    }
-    return lo;
-}
-
-// Header word of a record whose header did not fit the tile's LDS budget
-// (kept out of line: rare, and large when inlined).
-__device__ __noinline__ uint32_t header_word_slow(const onc_msg* d, uint32_t len, uint32_t meta, uint32_t k,
-                                                 const EncSrc* src) {
-    return header_word(*d, len, meta, k, *src);
-}
-
-constexpr int kHdrCap = 768;                  // header words staged per wave tile (3 KiB)
-constexpr int kMapCap = 512;                  // 64-byte output granules mapped per wave tile (32 KiB)
-constexpr uint16_t kNone16 = 0xFFFFu;
-
-// Per-record LDS entry, read with two ds_read_b128.
-struct RecEnt {
-    uint64_t start;     // first output byte
-    uint64_t pst;       // first payload byte (start + 4 * header words)
-    uint64_t en;        // one past the last byte
-    uint64_t srcbase;   // payload byte at output offset o lives at srcbase + o
-};
-
-// One wavefront's tile: kEmitRecs records, no workgroup barriers anywhere.
-struct WaveTile {
-    RecEnt ent[kEmitRecs + 1];       // [nrec] = sentinel {T1, T1, T1, 0}
-    uint32_t meta[kEmitRecs];        // plan_record() meta (header words etc.)
-    uint16_t hoff[kEmitRecs];        // staged header: word offset in hdr[], or kNone16
-    uint32_t hdr[kHdrCap];           // header words of the tile's records (stream order)
-    uint8_t map[kMapCap];            // granule g -> record holding byte 64*(G0+g) (or record 0)
-};
 
 // LDS writes of one lane become visible to the other lanes of the wave.
 __device__ __forceinline__ void wave_lds_sync() {
@@ -101,108 +60,12 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ int find_ent(const RecEnt* ent, int nrec, uint64_t x) {
-    int lo = 0, hi = nrec - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (ent[mid].start <= x) lo = mid;
-        else hi = mid - 1;
-    }
-    return lo;
-}
-
-__device__ __forceinline__ uint32_t hdr_word(const WaveTile& T, const EncArgs& a, const EncSrc& src, uint64_t r0,
-                                             int r, uint32_t len, uint32_t k) {
-    const uint16_t ho = T.hoff[r];
-    if (ho != kNone16) return T.hdr[ho + k];
-    return header_word_slow(a.msgs + r0 + r, len, T.meta[r], k, &src);
-}
-
-// Stream word k of tile record r; 0 outside [0, len).
-__device__ __forceinline__ uint32_t tile_word(const WaveTile& T, const EncArgs& a, const EncSrc& src,
-                                              uint64_t r0, int r, int64_t k) {
-    const RecEnt& e = T.ent[r];
-    const uint32_t len = uint32_t(e.en - e.start);
-    if (k < 0 || 4 * k >= int64_t(len)) return 0u;
-    const uint32_t hw = uint32_t((e.pst - e.start) >> 2);
-    if (uint64_t(k) < hw) return hdr_word(T, a, src, r0, r, len, uint32_t(k));
-    return load4_masked(e.srcbase + e.start + 4 * uint64_t(k), e.srcbase + e.en);
-}
-
-// Byte-granular: the 16 stream bytes of tile record r at output offsets
-// [o, o+16) (bytes outside the record read as 0).
-__device__ __forceinline__ void tile_chunk(const WaveTile& T, const EncArgs& a, const EncSrc& src, uint64_t r0,
-                                           int r, uint64_t o, uint32_t out[4]) {
-    const int64_t rel = int64_t(o) - int64_t(T.ent[r].start);
-    const int64_t k0 = rel >> 2;                 // floor division
-    const uint32_t sh = uint32_t(rel & 3);
-    uint32_t w[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) w[i] = tile_word(T, a, src, r0, r, k0 + i);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = funnel(w[i], w[i + 1], sh);
-}
-
-// Next record after r with bytes (skips zero-length records); nrec if none.
-__device__ __forceinline__ int next_rec(const WaveTile& T, int nrec, int r) {
-    ++r;
-    while (r < nrec && T.ent[r].en == T.ent[r].start) ++r;
-    return r;
-}
-
-// Byte-granular special chunk owned by r (tiles holding a record that does
-// not start or end on a 4-byte boundary: unpadded odd-length payloads).
-// Out of line: large, and rare in XDR traffic.
-__device__ __noinline__ void byte_chunk(const WaveTile* Tp, const EncArgs* ap, const EncSrc* srcp, uint64_t r0,
-                                        int nrec, int r, uint64_t o, uint32_t* v) {
-    const WaveTile& T = *Tp;
-    uint32_t w[4];
-    tile_chunk(T, *ap, *srcp, r0, r, o, w);
-    if (o + 16 > T.ent[r].en) {
-        const int r2 = next_rec(T, nrec, r);
-        if (r2 < nrec) {
-            // bytes outside a record read as 0, so the parts OR together
-            uint32_t b[4];
-            tile_chunk(T, *ap, *srcp, r0, r2, o, b);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) w[i] |= b[i];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = w[i];
-}
-
-// Word-aligned special chunk owned by r (every record of the tile starts
-// and ends on a 4-byte boundary and reads a 4-aligned payload): each output
-// dword is one whole stream word of r or of the next record.
-__device__ __forceinline__ void aligned_special(const WaveTile& T, const EncArgs& a, const EncSrc& src, uint64_t r0,
-                                                int nrec, int r, const RecEnt& e, uint64_t o, uint32_t v[4]) {
-    int rn = -1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint64_t p = o + 4 * i;
-        uint32_t w = 0;
-        if (p >= e.start && p < e.pst) {
-            w = hdr_word(T, a, src, r0, r, uint32_t(e.en - e.start), uint32_t((p - e.start) >> 2));
-        } else if (p >= e.pst && p < e.en) {
-            w = gload<uint32_t>(e.srcbase + p);
-        } else if (p >= e.en) {
-            // first words of the next record (always header: >= 24 B)
-            if (rn < 0) rn = next_rec(T, nrec, r);
-            if (rn < nrec) {
-                const RecEnt& f = T.ent[rn];
-                w = hdr_word(T, a, src, r0, rn, uint32_t(f.en - f.start), uint32_t((p - f.start) >> 2));
-            }
-        }
-        v[i] = w;
-    }
-}
-
+// Output bytes [lo, hi) of the 16-byte chunk at o (lo >= o, hi <= o + 16).
 __device__ __forceinline__ void store_chunk(uint8_t* out, uint64_t o, uint64_t lo, uint64_t hi, const uint32_t v[4]) {
     if (lo == o && hi == o + 16) {
         *reinterpret_cast<uint4*>(out + o) = make_uint4(v[0], v[1], v[2], v[3]);
     } else {
-        // Tile-boundary or capacity-boundary chunk: only this tile's bytes.
+        // Tile/span-boundary or capacity-boundary chunk: only this span's bytes.
         for (uint64_t bpos = lo; bpos < hi; ++bpos) {
             const uint32_t j = uint32_t(bpos - o);
             out[bpos] = uint8_t(v[j >> 2] >> (8 * (j & 3)));
@@ -210,98 +73,23 @@ __device__ __forceinline__ void store_chunk(uint8_t* out, uint64_t o, uint64_t l
     }
 }
 
-// enc_fixup: the tiles enc_emit deferred (a record that is not 4-byte
-// aligned — unpadded odd-length payloads — or headers beyond the fast
-// kernel's LDS budget). One wavefront per tile, single chunk pass: every
-// chunk (payload-only or special) is computed by its lane and all chunks of
-// a step are stored by one global_store_dwordx4, so 128-byte lines are
-// always written whole.
-__global__ __launch_bounds__(kTile) void enc_fixup_kernel(EncArgs a) {
-    __shared__ WaveTile s_tiles[kTile / 64];
-    const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    WaveTile& T = s_tiles[wv];
-    const uint32_t ndef = *a.defer_count;
-    const uint64_t nwaves = uint64_t(gridDim.x) * (kTile / 64);
-    const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena),
-                     reinterpret_cast<uintptr_t>(a.payload_arena)};
-    for (uint64_t i = uint64_t(blockIdx.x) * (kTile / 64) + wv; i < ndef; i += nwaves) {
-        const uint64_t tile = a.defer_list[i];
-        const uint64_t r0 = tile * kEmitRecs;
-        const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
-        const uint64_t tile_base = a.tile_base[tile];
-        wave_lds_sync();   // the previous tile's readers are done with T
-
-        uint64_t len = 0, srcbase = 0;
-        uint32_t hw = 0;
-        bool word_aligned = true;
-        uint64_t start, en, pst;
-        {
-            onc_msg d;
-            uint32_t meta = 0;
-            if (lane < nrec) {
-                d = a.msgs[r0 + lane];
-                const RecPlan p = plan_record(d, a.unix);
-                len = p.len;
-                meta = p.meta;
-                hw = len ? meta_hw(meta) : 0;
-                word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((src.payload_arena + d.payload_off) & 3) == 0);
-            }
-            const uint64_t v = (len << 16) | hw;
-            const uint64_t incl = wave_incl_scan_u64(v);
-            const uint64_t excl = incl - v;
-            start = tile_base + (excl >> 16);
-            en = start + len;
-            pst = start + 4ull * hw;
-            const uint32_t hoff = uint32_t(excl & 0xFFFFu);
-            if (lane < nrec) {
-                srcbase = src.payload_arena + d.payload_off - pst;
-                T.ent[lane] = RecEnt{start, pst, en, srcbase};
-                T.meta[lane] = meta;
-                const bool staged = hoff + hw <= uint32_t(kHdrCap);
-                T.hoff[lane] = staged ? uint16_t(hoff) : kNone16;
-                if (len != 0 && staged) put_header_words(d, uint32_t(len), src, &T.hdr[hoff]);
-            }
-        }
-        const uint64_t T0 = tile_base;
-        const uint64_t T1 = __shfl(en, nrec - 1, 64);
-        const uint64_t G0 = T0 >> 6;
-        if (lane < nrec && len != 0) {
-            const uint64_t g_hi = min((en - 1) >> 6, G0 + kMapCap - 1);
-            for (uint64_t g = (start + 63) >> 6; g <= g_hi; ++g) T.map[g - G0] = uint8_t(lane);
-        }
-        if (lane == 0) {
-            T.ent[nrec] = RecEnt{T1, T1, T1, 0};
-            if (T0 & 63) T.map[0] = 0;
-        }
-        const bool tile_aligned = __all(word_aligned) && (T0 & 3) == 0;
-        wave_lds_sync();
-
-        const uint64_t E = min(T1, a.out_cap);
-        if (E <= T0) continue;
-        for (uint64_t c = (T0 >> 4) + lane; c < (E + 15) >> 4; c += 64) {
-            const uint64_t o = c << 4;
-            const uint64_t lo = max(o, T0);
-            const uint64_t g = (lo >> 6) - G0;
-            int r = g < uint64_t(kMapCap) ? int(T.map[g]) : find_ent(T.ent, nrec, lo);
-            RecEnt e = T.ent[r];
-            while (lo >= e.en && r + 1 < nrec) e = T.ent[++r];
-            uint32_t v[4];
-            if (o >= e.pst && o + 16 <= e.en) load16_unaligned(e.srcbase + o, v);
-            else if (tile_aligned) aligned_special(T, a, src, r0, nrec, r, e, o, v);
-            else byte_chunk(&T, &a, &src, r0, nrec, r, o, v);
-            store_chunk(a.out, o, lo, min(o + 16, E), v);
-        }
-    }
+// Byte offset of tile `tile` in the output: base of its enc_len workgroup
+// (scan of the workgroup totals) + totals of the tiles before it there.
+__device__ __forceinline__ uint64_t tile_start(const EncArgs& a, uint64_t tile) {
+    const uint64_t blk = tile / (kTile / kEmitRecs);
+    uint64_t T0 = a.block_base[blk];
+    for (uint64_t t = blk * (kTile / kEmitRecs); t < tile; ++t) T0 += a.tile_sum[t];
+    return T0;
 }
 
 // ---------------------------------------------------------------------------
-// enc_emit: the hot kernel.
+// enc_emit: the hot kernel (word-aligned tiles).
 // ---------------------------------------------------------------------------
-constexpr int kFastHdrCap = 1024;             // header words per wave tile (4 KiB of LDS)
+constexpr int kFastHdrCap = 2048;             // header words per wave tile (8 KiB of LDS)
 constexpr int kFastMapCap = 1024;             // output granules per wave tile
+constexpr int kFastWaves = 4;                 // wave tiles per workgroup
 
-// Per-record LDS entry of the fast kernel (two ds_read_b128).
+// Per-record LDS entry of enc_emit (two ds_read_b128).
 struct FastEnt {
     uint64_t pst;       // first payload byte
     uint64_t en;        // one past the last byte
@@ -324,8 +112,9 @@ struct FastTile {
 //  bytes and LDS header words; each record writes its LDS entry, serialises
 //  its header words into LDS, and claims its output granules in the
 //  granule map (granule = 64 B, doubled until the tile fits the map).
-//  Tiles whose records are not all 4-byte aligned, or whose headers exceed
-//  the LDS budget, are appended to the deferred list for enc_fixup.
+//  Tiles whose records are not all 4-byte aligned (unpadded odd-length
+//  payloads), or whose headers exceed the LDS budget, are flagged for
+//  enc_fixup in tile_base.
 //  Chunk pass (lane per 16-byte output chunk, 1 KiB contiguous per wave):
 //  granule map -> record entry; a chunk inside its record's payload is one
 //  unaligned 16-byte load; any other chunk takes each of its four dwords
@@ -335,35 +124,28 @@ struct FastTile {
 //  (a line left partially written costs a read-modify-write at eviction).
 //  Chunks straddling a tile boundary are written with byte stores of only
 //  this tile's bytes, so tiles never exchange data.
-// kLab != 0 only in tools/emit_lab.hip.
-template <int kLab>
-__global__ __launch_bounds__(kTile) void enc_emit_kernel_t(EncArgs a) {
-    __shared__ FastTile s_tiles[kTile / 64];
+__global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel(EncArgs a) {
+    __shared__ FastTile s_tiles[kFastWaves];
 
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    const uint64_t tile = uint64_t(blockIdx.x) * (kTile / 64) + wv;
+    const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + wv;
     const uint64_t r0 = tile * kEmitRecs;
     if (r0 >= a.n) return;
-    // tile base = workgroup base (scan of enc_len's workgroup totals) + the
-    // totals of the tiles before this one in the workgroup
-    uint64_t T0 = a.block_base[blockIdx.x];
-    for (int w = 0; w < wv; ++w) T0 += a.tile_sum[uint64_t(blockIdx.x) * (kTile / 64) + w];
-    if (lane == 0) a.tile_base[tile] = T0;            // read by enc_fixup
+    const uint64_t T0 = tile_start(a, tile);
     FastTile& T = s_tiles[wv];
     const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
     const uintptr_t payload = reinterpret_cast<uintptr_t>(a.payload_arena);
 
     onc_msg d;
     uint64_t len = 0;
-    uint32_t meta = 0, hw = 0;
+    uint32_t hw = 0;
     bool word_aligned = true;
     if (lane < nrec) {
         d = a.msgs[r0 + lane];
         const RecPlan p = plan_record(d, a.unix);
         len = p.len;
-        meta = p.meta;
-        hw = len ? meta_hw(meta) : 0;
+        hw = len ? meta_hw(p.meta) : 0;
         word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((payload + d.payload_off) & 3) == 0);
     }
     // One wave scan places output bytes and LDS header words: (len << 16 | hw).
@@ -381,10 +163,8 @@ __global__ __launch_bounds__(kTile) void enc_emit_kernel_t(EncArgs a) {
         if (len != 0 && en > a.out_cap) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
     }
     const bool fast = __all(word_aligned) && (T0 & 3) == 0 && (last & 0xFFFFu) <= uint64_t(kFastHdrCap);
-    if (!fast) {
-        if (lane == 0) a.defer_list[atomicAdd(a.defer_count, 1u)] = uint32_t(tile);
-        return;
-    }
+    if (lane == 0) a.tile_base[tile] = T0 | (fast ? 0 : kDeferBit);
+    if (!fast) return;
     const int32_t dw = int32_t(hoff) - int32_t((start - T0) >> 2);
     const int32_t dwn_raw = __shfl_down(dw, 1, 64);
     if (lane < nrec) {
@@ -411,6 +191,7 @@ __global__ __launch_bounds__(kTile) void enc_emit_kernel_t(EncArgs a) {
     wave_lds_sync();
 
     const uint64_t E = min(T1, a.out_cap);
+    if (E <= T0) return;                              // no bytes (all records failed, or beyond out_cap)
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.msgs);   // >= 64 valid bytes
     for (uint64_t c = (T0 >> 4) + lane; c < (E + 15) >> 4; c += 64) {
         const uint64_t o = c << 4;
@@ -438,6 +219,167 @@ __global__ __launch_bounds__(kTile) void enc_emit_kernel_t(EncArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// enc_fixup: byte-general path for the tiles enc_emit flagged.
+// ---------------------------------------------------------------------------
+constexpr int kImgCap = 2048;                 // header image dwords per span (8 KiB of LDS)
+constexpr int kSubRecs = 16;                  // records per span when a tile's image exceeds kImgCap
+// a record's header is at most 7 + 2 * (2 + 50) words (Call with two 200-byte
+// auth bodies), plus one image word for an unaligned start
+static_assert(kSubRecs * (7 + 2 * 52 + 1) <= kImgCap, "a span of maximal headers must fit LDS");
+
+// Per-record LDS entry of enc_fixup (two ds_read_b128).
+struct GenEnt {
+    uint64_t pst;       // first payload byte (output offset)
+    uint64_t en;        // one past the last byte
+    uint64_t srcbase;   // payload byte at output offset o lives at srcbase + o
+    int32_t ib;         // image dword of output dword q: (q - (S0 >> 2)) + ib
+    int32_t pad;
+};
+
+struct GenTile {
+    GenEnt ent[kEmitRecs + 1];       // [span records] = sentinel {S1, S1, 0, 0}
+    uint32_t img[kImgCap];           // header bytes at their output-dword positions, zero elsewhere
+    uint8_t map[kFastMapCap];        // granule -> span record holding its first byte
+};
+
+// One span (records [lo_rec, hi_rec) of the tile, bytes [S0, S1)) of the
+// general path. Per record: its header serialised into the LDS image already
+// shifted to its output byte alignment (start & 3; bytes outside the header
+// are zero), so an output dword's header bytes are one image word; payload
+// bytes come from the five aligned source dwords under the chunk, each
+// clamped into the dwords that hold this chunk's payload bytes (nothing
+// outside the payload is touched), combined by v_alignbyte. An output dword
+// is the OR of (this record's image word, the next record's image word,
+// this record's masked payload bytes): a 16-byte chunk meets at most one
+// payload, since every record has >= 24 header bytes.
+__device__ __forceinline__ void gen_span(GenTile& T, const EncArgs& a, const onc_msg& d, int lane, int lo_rec,
+                                         int hi_rec, uint64_t len, uint32_t hw, uint64_t start, uint64_t S0,
+                                         uint64_t S1) {
+    const uintptr_t payload = reinterpret_cast<uintptr_t>(a.payload_arena);
+    const bool active = lane >= lo_rec && lane < hi_rec;
+    const uint64_t en = start + len;
+    const uint64_t pst = start + 4ull * hw;
+    const uint32_t m = uint32_t(start & 3);
+    const uint32_t iw = active && len ? hw + (m ? 1u : 0u) : 0u;
+    const uint64_t iincl = wave_incl_scan_u64(iw);
+    const uint32_t ibase = uint32_t(iincl - iw);
+    const int j = lane - lo_rec;
+    const int nspan = hi_rec - lo_rec;
+    if (active) {
+        const int32_t ib = int32_t(ibase) - int32_t((start >> 2) - (S0 >> 2));
+        T.ent[j] = GenEnt{pst, en, payload + d.payload_off - pst, ib, 0};
+        if (len != 0) {
+            const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
+            if (m == 0) {
+                WordSink w{&T.img[ibase]};
+                put_header_words(d, uint32_t(len), src, w);
+            } else {
+                ShiftSink w{&T.img[ibase], 0u, 4u - m};
+                put_header_words(d, uint32_t(len), src, w);
+                w.finish();
+            }
+        }
+    }
+    uint32_t gs = 6;
+    while (((S1 - S0) >> gs) >= uint64_t(kFastMapCap)) ++gs;
+    const uint64_t G0 = S0 >> gs;
+    if (active && len != 0) {
+        const uint64_t gsz = 1ull << gs;
+        for (uint64_t g = (start + gsz - 1) >> gs; g <= (en - 1) >> gs; ++g) T.map[g - G0] = uint8_t(j);
+    }
+    if (lane == 0) {
+        T.ent[nspan] = GenEnt{S1, S1, 0, 0, 0};
+        if (S0 & ((1ull << gs) - 1)) T.map[0] = 0;
+    }
+    wave_lds_sync();
+
+    const uint64_t E = min(S1, a.out_cap);
+    if (E <= S0) return;                              // no bytes (all records failed, or beyond out_cap)
+    const int64_t q0 = int64_t(S0 >> 2);
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.msgs);
+    for (uint64_t c = (S0 >> 4) + lane; c < (E + 15) >> 4; c += 64) {
+        const uint64_t o = c << 4;
+        const uint64_t lo = max(o, S0);
+        int r = T.map[(lo >> gs) - G0];
+        GenEnt e = T.ent[r];
+        while (lo >= e.en) e = T.ent[++r];            // sentinel en = S1 > lo
+        const uint64_t b0 = max(o, e.pst), b1 = min(o + 16, e.en);
+        const bool hp = b0 < b1;
+        const bool whole = o >= e.pst && o + 16 <= e.en;
+        const uintptr_t sb = e.srcbase + o;
+        const uintptr_t base = sb & ~uintptr_t(3);
+        const uint32_t sh = uint32_t(sb & 3);
+        const uintptr_t first = hp ? ((e.srcbase + b0) & ~uintptr_t(3)) : dummy;
+        const uintptr_t last = hp ? ((e.srcbase + b1 - 1) & ~uintptr_t(3)) : dummy;
+        uint32_t w[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            uintptr_t ad = base + 4 * k;
+            ad = ad < first ? first : (ad > last ? last : ad);
+            w[k] = gload<uint32_t>(ad);
+        }
+        uint32_t v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = funnel(w[i], w[i + 1], sh);
+        if (!whole) {
+            const int32_t ibn = T.ent[r + 1].ib;
+            const int64_t q = int64_t(o >> 2) - q0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint64_t p = o + 4 * i;
+                const int64_t h0 = q + i + e.ib, h1 = q + i + ibn;
+                const uint32_t x0 = T.img[h0 < 0 ? 0 : (h0 >= kImgCap ? kImgCap - 1 : h0)];
+                const uint32_t x1 = T.img[h1 < 0 ? 0 : (h1 >= kImgCap ? kImgCap - 1 : h1)];
+                // the next record's header (none past the span's last byte)
+                const uint32_t hv = (p < e.pst ? x0 : 0u) | (p + 4 > e.en && e.en < S1 ? x1 : 0u);
+                const int64_t l8 = int64_t(b0) - int64_t(p), h8 = int64_t(b1) - int64_t(p);
+                const uint32_t l = uint32_t(l8 < 0 ? 0 : (l8 > 4 ? 4 : l8));
+                const uint32_t h = uint32_t(h8 < 0 ? 0 : (h8 > 4 ? 4 : h8));
+                const uint32_t pm = hp ? uint32_t(((1ull << (8 * h)) - 1ull) & ~((1ull << (8 * l)) - 1ull)) : 0u;
+                v[i] = hv | (v[i] & pm);
+            }
+        }
+        store_chunk(a.out, o, lo, min(o + 16, E), v);
+    }
+}
+
+// enc_fixup: one wavefront (= workgroup) per tile; tiles enc_emit handled
+// exit after reading their flag.
+__global__ __launch_bounds__(64) void enc_fixup_kernel(EncArgs a) {
+    __shared__ GenTile T;
+    const int lane = threadIdx.x;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t tb = a.tile_base[tile];
+    if (!(tb & kDeferBit)) return;
+    const uint64_t T0 = tb & ~kDeferBit;
+    const uint64_t r0 = tile * kEmitRecs;
+    const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
+
+    onc_msg d;
+    uint64_t len = 0;
+    uint32_t hw = 0;
+    if (lane < nrec) {
+        d = a.msgs[r0 + lane];
+        const RecPlan p = plan_record(d, a.unix);
+        len = p.len;
+        hw = len ? meta_hw(p.meta) : 0;
+    }
+    const uint64_t incl = wave_incl_scan_u64(len);
+    const uint64_t start = T0 + incl - len;
+    // image words of the whole tile (upper bound: one extra per record)
+    const uint64_t iall = wave_incl_scan_u64(len ? hw + 1 : 0);
+    const bool split = __shfl(iall, nrec - 1, 64) > uint64_t(kImgCap);
+    const int step = split ? kSubRecs : kEmitRecs;
+    for (int lo_rec = 0; lo_rec < nrec; lo_rec += step) {
+        const int hi_rec = min(nrec, lo_rec + step);
+        const uint64_t S0 = __shfl(start, lo_rec, 64);
+        const uint64_t S1 = __shfl(start + len, hi_rec - 1, 64);
+        if (lo_rec) wave_lds_sync();                   // previous span's readers are done
+        gen_span(T, a, d, lane, lo_rec, hi_rec, len, hw, start, S0, S1);
+    }
+}
+
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
     const uint64_t tiles = num_tiles(a.n);
     hipLaunchKernelGGL(enc_len_kernel, dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
@@ -445,15 +387,13 @@ hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
-    const uint64_t blocks = (num_emit_tiles(a.n) + kTile / 64 - 1) / (kTile / 64);
-    hipLaunchKernelGGL(enc_emit_kernel_t<0>, dim3(uint32_t(blocks)), dim3(kTile), 0, s, a);
+    const uint64_t blocks = (num_emit_tiles(a.n) + kFastWaves - 1) / kFastWaves;
+    hipLaunchKernelGGL(enc_emit_kernel, dim3(uint32_t(blocks)), dim3(64 * kFastWaves), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_enc_fixup(const EncArgs& a, hipStream_t s) {
-    uint64_t blocks = (num_emit_tiles(a.n) + kTile / 64 - 1) / (kTile / 64);
-    if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(enc_fixup_kernel, dim3(uint32_t(blocks)), dim3(kTile), 0, s, a);
+    hipLaunchKernelGGL(enc_fixup_kernel, dim3(uint32_t(num_emit_tiles(a.n))), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

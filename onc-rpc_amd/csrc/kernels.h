@@ -22,9 +22,7 @@ struct EncArgs {
     int32_t* status;        // n
     uint32_t* rec_len;      // n, optional
     uint64_t* tile_sum;     // tiles
-    uint64_t* tile_base;    // tiles (written by enc_emit, read by enc_fixup)
-    uint32_t* defer_list;   // tiles: tiles enc_emit left to enc_fixup
-    uint32_t* defer_count;  // zeroed by enc_len
+    uint64_t* tile_base;    // tiles: byte offset | bit 63 = left to enc_fixup (written by enc_emit)
     uint64_t* block_sum;    // enc_len workgroups (256 records): byte totals
     uint64_t* block_base;   // exclusive scan of block_sum
 };

@@ -28,6 +28,7 @@ EXPORTED = [
     "onc_codec_sync", "onc_codec_reserve", "onc_codec_last_error", "onc_status_str",
     "onc_codec_enable_timing", "onc_codec_kernel_stats", "onc_codec_reset_stats",
     "onc_kernel_name", "onc_encode_lengths", "onc_encode", "onc_decode", "onc_scan_lengths",
+    "onc_expected_message_len",
 ]
 
 
@@ -73,10 +74,20 @@ def load_library(path=LIB_PATH):
     lib.onc_encode.argtypes = [vp, C.POINTER(OncBatch), vp, u64, vp, vp, vp]
     lib.onc_decode.argtypes = [vp, vp, vp, u64, i32, C.POINTER(OncDecoded)]
     lib.onc_scan_lengths.argtypes = [vp, vp, u64, u64, vp]
+    lib.onc_expected_message_len.argtypes = [C.c_char_p, u64, C.POINTER(C.c_uint32)]
+    lib.onc_expected_message_len.restype = C.c_int32
     for name in EXPORTED:
         getattr(lib, name).restype = getattr(lib, name).restype or i32
     _LIB = lib
     return lib
+
+
+def expected_message_len(buf: bytes):
+    """expected_message_len (src/rpc_message.rs:343-367) -> (status, length)."""
+    lib = load_library()
+    out = C.c_uint32(0)
+    st = lib.onc_expected_message_len(buf, len(buf), C.byref(out))
+    return st, out.value
 
 
 def _ptr(t):

@@ -1001,6 +1001,68 @@ void oracle_decode_batch_mt(const uint8_t* wire, const uint64_t* rec_off, uint64
     for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
 }
 
+/* Multi-threaded batch encode (CPU-baseline leg only): what a multi-core
+ * caller of the reference does — serialised_len() per record
+ * (src/rpc_message.rs:201-204) on every thread, an exclusive scan of the
+ * lengths, then serialise_into() of each thread's contiguous record range
+ * into its own region of the shared buffer. Same outputs as
+ * oracle_encode_batch when out_cap covers the total. */
+typedef struct {
+    uint64_t lo, hi;
+    const onc_msg* msgs;
+    const onc_unix_params* unix_table;
+    const uint8_t *auth_arena, *payload_arena;
+    uint8_t* out;
+    uint64_t* rec_off;
+    int32_t* status;
+    uint32_t* rec_len;
+    int phase;
+} encode_job;
+
+static void* encode_thread(void* arg) {
+    encode_job* j = (encode_job*)arg;
+    for (uint64_t i = j->lo; i < j->hi; i++) {
+        uint64_t written = 0, slen = 0;
+        if (j->phase == 0) {
+            int32_t st = oracle_encode_message(&j->msgs[i], j->unix_table, j->auth_arena,
+                                               j->payload_arena, NULL, 0, &written, &slen);
+            j->rec_len[i] = (st == ONC_OK || st == ONC_ENC_WRITE_ZERO) ? (uint32_t)slen : 0;
+        } else {
+            const uint64_t off = j->rec_off[i];
+            j->status[i] = oracle_encode_message(&j->msgs[i], j->unix_table, j->auth_arena,
+                                                 j->payload_arena, j->out + off, j->rec_len[i],
+                                                 &written, &slen);
+        }
+    }
+    return NULL;
+}
+
+void oracle_encode_batch_mt(uint64_t n, const onc_msg* msgs, const onc_unix_params* unix_table,
+                            const uint8_t* auth_arena, const uint8_t* payload_arena, uint8_t* out,
+                            uint64_t* rec_off, int32_t* status, uint32_t* rec_len, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    encode_job jobs[256];
+    for (int phase = 0; phase < 2; phase++) {
+        if (phase == 1) {
+            uint64_t off = 0;
+            for (uint64_t i = 0; i < n; i++) {
+                rec_off[i] = off;
+                off += rec_len[i];
+            }
+            rec_off[n] = off;
+        }
+        for (int t = 0; t < threads; t++) {
+            encode_job j = {n * t / threads, n * (t + 1) / threads, msgs, unix_table, auth_arena,
+                            payload_arena, out, rec_off, status, rec_len, phase};
+            jobs[t] = j;
+            pthread_create(&tid[t], NULL, encode_thread, &jobs[t]);
+        }
+        for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+    }
+}
+
 int32_t oracle_expected_message_len(const uint8_t* data, uint64_t len, uint32_t* out) {
     uint32_t want = 0;
     o_err e = expected_message_len(data, len, &want);

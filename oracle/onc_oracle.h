@@ -60,6 +60,13 @@ void oracle_decode_batch_mt(const uint8_t* wire, const uint64_t* rec_off, uint64
                             onc_msg* msgs, onc_unix_params* unix_params, int32_t* status,
                             uint32_t* aux0, uint32_t* aux1, int threads);
 
+/* Multi-threaded encode (CPU-baseline leg only): per-record lengths on all
+ * threads, exclusive scan, then each thread serialises its contiguous range.
+ * `out` must hold the total (no capacity handling). */
+void oracle_encode_batch_mt(uint64_t n, const onc_msg* msgs, const onc_unix_params* unix_table,
+                            const uint8_t* auth_arena, const uint8_t* payload_arena, uint8_t* out,
+                            uint64_t* rec_off, int32_t* status, uint32_t* rec_len, int threads);
+
 /* Component-level entry points used by the golden-vector tests. */
 /* expected_message_len — src/rpc_message.rs:343-367 */
 int32_t oracle_expected_message_len(const uint8_t* data, uint64_t len, uint32_t* out);

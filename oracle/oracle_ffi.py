@@ -32,6 +32,8 @@ def load():
     lib.oracle_decode_batch.restype = None
     lib.oracle_decode_batch_mt.argtypes = [vp, vp, u64, i32, vp, vp, vp, vp, vp, i32]
     lib.oracle_decode_batch_mt.restype = None
+    lib.oracle_encode_batch_mt.argtypes = [u64, vp, vp, vp, vp, vp, vp, vp, vp, i32]
+    lib.oracle_encode_batch_mt.restype = None
     lib.oracle_expected_message_len.argtypes = [vp, u64, vp]
     lib.oracle_expected_message_len.restype = C.c_int32
     lib.oracle_auth_decode.argtypes = [vp, u64, i32, vp, vp, vp]
@@ -82,6 +84,22 @@ def encode_batch(hb, out_cap=None):
                             _p(out), out_cap, _p(rec_off), _p(status), _p(rec_len))
     total = min(int(rec_off[n]), out_cap)
     return out[:total].tobytes(), rec_off, status[:n], rec_len[:n]
+
+
+def encode_batch_mt(hb, threads, out=None):
+    """Multi-threaded encode (CPU-baseline leg): -> (out array, rec_off, status, rec_len).
+    `out` (uint8) is reused when large enough."""
+    lib = load()
+    n = hb.n
+    rec_off = np.zeros(n + 1, np.uint64)
+    status = np.zeros(max(n, 1), np.int32)
+    rec_len = np.zeros(max(n, 1), np.uint32)
+    if out is None:
+        _, off, _, _ = encode_batch(hb)
+        out = np.zeros(max(int(off[n]), 1), np.uint8)
+    lib.oracle_encode_batch_mt(n, _p(hb.msgs), _p(hb.unix), _p(hb.auth_arena), _p(hb.payload_arena),
+                               _p(out), _p(rec_off), _p(status), _p(rec_len), threads)
+    return out, rec_off, status[:n], rec_len[:n]
 
 
 def decode_batch(wire, rec_off, mode, threads=1):

@@ -1,0 +1,344 @@
+// test_mirror.cpp — the reference's own unit tests, restated against the C++
+// mirror types (include/onc_rpc.hpp) running on the GPU codec.
+//
+// Each test names the reference test it follows. Byte vectors are read from
+// tests/golden/vectors.json (fixtures extracted from the reference's tests,
+// see tests/golden/make_golden.py). Run by tests/test_cpp_mirror.py (-m gpu).
+//
+// Usage: test_mirror <path to vectors.json>
+#include <cstdio>
+#include <fstream>
+#include <functional>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/onc_rpc.hpp"
+
+using namespace onc_rpc;
+
+static int g_fail = 0, g_pass = 0;
+#define CHECK(cond)                                                                  \
+    do {                                                                             \
+        if (!(cond)) {                                                               \
+            std::fprintf(stderr, "%s:%d CHECK failed: %s\n", __FILE__, __LINE__, #cond); \
+            throw std::runtime_error("check failed");                                \
+        }                                                                            \
+    } while (0)
+
+// ---- minimal fixture reader: the entry whose "name" is `name` ------------------
+static std::string g_json;
+
+static std::string entry(const std::string& name) {
+    const std::string key = "\"name\": \"" + name + "\"";
+    const size_t a = g_json.find(key);
+    if (a == std::string::npos) throw std::runtime_error("no fixture " + name);
+    size_t b = g_json.find("\"name\": \"", a + key.size());
+    return g_json.substr(a, b == std::string::npos ? std::string::npos : b - a);
+}
+
+static std::string field_str(const std::string& e, const std::string& f) {
+    const std::string key = "\"" + f + "\": \"";
+    const size_t a = e.find(key);
+    if (a == std::string::npos) throw std::runtime_error("no field " + f);
+    const size_t s = a + key.size();
+    return e.substr(s, e.find('"', s) - s);
+}
+
+static long field_int(const std::string& e, const std::string& f) {
+    const std::string key = "\"" + f + "\": ";
+    const size_t a = e.find(key);
+    if (a == std::string::npos) throw std::runtime_error("no field " + f);
+    return std::stol(e.substr(a + key.size()));
+}
+
+static std::vector<uint8_t> unhex(const std::string& h) {
+    std::vector<uint8_t> v(h.size() / 2);
+    for (size_t i = 0; i < v.size(); ++i) v[i] = uint8_t(std::stoi(h.substr(2 * i, 2), nullptr, 16));
+    return v;
+}
+
+static std::vector<uint8_t> fixture(const std::string& name) { return unhex(field_str(entry(name), "hex")); }
+
+static std::vector<uint32_t> gids16() {
+    return {501, 12, 20, 61, 79, 80, 81, 98, 701, 33, 100, 204, 250, 395, 398, 399};
+}
+
+// ---- tests ----------------------------------------------------------------------
+
+// rpc_message.rs:446-580 test_rpcmessage_auth_unix (+ Bytes variant :582-719)
+static void test_rpcmessage_auth_unix(Codec& c) {
+    const std::vector<uint8_t> raw = fixture("call_auth_unix_16gids_288B");
+    for (DecodeMode mode : {DecodeMode::Slice, DecodeMode::Bytes}) {
+        const RpcMessage msg = RpcMessage::try_from(c, Bytes(raw), mode);
+        CHECK(msg.xid() == 643743997);
+        CHECK(msg.serialised_len(c) == 288);
+        const CallBody* body = msg.call_body();
+        CHECK(body != nullptr && msg.reply_body() == nullptr);
+        CHECK(body->rpc_version() == 2);
+        CHECK(body->program() == 100003);
+        CHECK(body->program_version() == 4);
+        CHECK(body->procedure() == 1);
+        CHECK(body->auth_credentials().kind() == AuthFlavor::Kind::AuthUnix);
+        const AuthUnixParams& p = body->auth_credentials().unix_params();
+        CHECK(p.stamp() == 0);
+        CHECK(p.machine_name().len == 0);
+        CHECK(p.uid() == 501);
+        CHECK(p.gid() == 20);
+        CHECK(p.gids().has_value() && *p.gids() == gids16());
+        CHECK(body->auth_verifier() == AuthFlavor::none());
+        CHECK(body->payload().len == 288 - 4 - 4 - 4 - 16 - 92 - 8);
+        // borrowed, zero-copy: the payload view points into `raw`
+        CHECK(body->payload().ptr == raw.data() + (288 - body->payload().len));
+        // re-serialise -> identical bytes
+        CHECK(msg.serialise(c) == raw);
+    }
+}
+
+// rpc_message.rs:790-796 (call with one gid; also benches/bench.rs:55-60)
+static void test_rpcmessage_auth_unix_1gid(Codec& c) {
+    const std::vector<uint8_t> raw = fixture("call_auth_unix_1gid_156B");
+    const RpcMessage msg = RpcMessage::try_from(c, Bytes(raw));
+    CHECK(msg.xid() == 643744006);
+    CHECK(msg.call_body()->auth_credentials().unix_params().gids() == std::vector<uint32_t>{0});
+    CHECK(msg.serialise(c) == raw);
+}
+
+// rpc_message.rs:849-853 test_rpcmessage_reply (accepted success)
+static void test_rpcmessage_reply(Codec& c) {
+    const std::vector<uint8_t> raw = fixture("reply_accepted_success_76B");
+    for (DecodeMode mode : {DecodeMode::Slice, DecodeMode::Bytes}) {
+        const RpcMessage msg = RpcMessage::try_from(c, Bytes(raw), mode);
+        CHECK(msg.xid() == 643743997);
+        const ReplyBody* r = msg.reply_body();
+        CHECK(r != nullptr && r->is_accepted());
+        CHECK(r->accepted()->auth_verifier() == AuthFlavor::none());
+        CHECK(r->accepted()->status().kind() == AcceptedStatus::Kind::Success);
+        CHECK(r->accepted()->status().payload().len == 48);
+        CHECK(msg.serialised_len(c) == 76);
+        CHECK(msg.serialise(c) == raw);
+    }
+}
+
+// rpc_message.rs:937-940 (fuzz-found reply with trailing bytes) and the
+// unwrap_header error vectors (:388-427): exact Error variant and payload.
+static void test_error_vectors(Codec& c) {
+    for (const char* name : {"fuzz_reply_too_long_for_type_39B", "unwrap_header_incomplete_header",
+                             "unwrap_header_incomplete_message", "unwrap_header_fragmented"}) {
+        const std::string e = entry(name);
+        const std::vector<uint8_t> raw = unhex(field_str(e, "hex"));
+        const long want = field_int(e, "status");
+        for (DecodeMode mode : {DecodeMode::Slice, DecodeMode::Bytes}) {
+            bool threw = false;
+            try {
+                (void)RpcMessage::try_from(c, Bytes(raw), mode);
+            } catch (const Error& err) {
+                threw = true;
+                CHECK(err.code() == want);
+                if (want == ONC_ERR_INCOMPLETE_MESSAGE) {
+                    CHECK(err.buffer_len() == uint32_t(field_int(e, "aux0")));
+                    CHECK(err.expected() == uint32_t(field_int(e, "aux1")));
+                }
+            }
+            CHECK(threw);
+        }
+    }
+}
+
+// rpc_message.rs:171-190 doc example: CallBody with AuthNone x2, no payload.
+static void test_doc_example(Codec& c) {
+    const std::vector<uint8_t> want = fixture("doc_example_call_none_none_empty");
+    const RpcMessage msg(4242, MessageType::call(CallBody(100000, 42, 13, AuthFlavor::none(), AuthFlavor::none(),
+                                                          Bytes())));
+    CHECK(msg.serialised_len(c) == want.size());
+    CHECK(msg.serialise(c) == want);
+    // serialise_into appends (a Cursor positioned at the end of a Vec)
+    std::vector<uint8_t> buf = {0xAA};
+    msg.serialise_into(c, buf);
+    CHECK(buf.size() == want.size() + 1 && buf[0] == 0xAA);
+    CHECK(std::vector<uint8_t>(buf.begin() + 1, buf.end()) == want);
+}
+
+// benches/bench.rs:86-101: the reference benchmark's round trip (configs[0]).
+static void test_bench_message_round_trip(Codec& c) {
+    std::vector<uint8_t> payload(64);
+    for (size_t i = 0; i < payload.size(); ++i) payload[i] = uint8_t(i * 7 + 3);
+    const RpcMessage msg(4242, MessageType::call(CallBody(
+                                   100000, 42, 13, AuthFlavor::unix(AuthUnixParams(0, Bytes(), 501, 20, gids16())),
+                                   AuthFlavor::none(), Bytes(payload))));
+    const std::vector<uint8_t> wire = msg.serialise(c);
+    CHECK(wire.size() == 192);   // W = 192
+    const RpcMessage back = RpcMessage::try_from(c, Bytes(wire));
+    CHECK(back.xid() == msg.xid());
+    CHECK(back.call_body()->auth_credentials() == msg.call_body()->auth_credentials());
+    CHECK(back.call_body()->payload() == Bytes(payload));
+    CHECK(back == msg);
+}
+
+// Panic parity: flavor.rs:110 (assoc > 200), unix_params.rs:149 (name > 255),
+// unix_params.rs:47 (> 16 gids) -> std::logic_error.
+static void test_panics(Codec& c) {
+    bool threw = false;
+    try {
+        AuthUnixParams(0, Bytes(), 0, 0, std::vector<uint32_t>(17, 1));
+    } catch (const std::logic_error&) {
+        threw = true;
+    }
+    CHECK(threw);
+    std::vector<uint8_t> big(256, 'x');
+    threw = false;
+    try {
+        AuthUnixParams(0, Bytes(big), 0, 0, {});
+    } catch (const std::logic_error&) {
+        threw = true;
+    }
+    CHECK(threw);
+    // 201 bytes of AuthNone data: the reference panics in serialise_into
+    std::vector<uint8_t> body(201, 1);
+    const RpcMessage m(1, MessageType::call(CallBody(1, 1, 1, AuthFlavor::none(Bytes(body)), AuthFlavor::none(),
+                                                     Bytes())));
+    threw = false;
+    try {
+        (void)m.serialise(c);
+    } catch (const std::logic_error&) {
+        threw = true;
+    }
+    CHECK(threw);
+    // exactly 200 is fine (flavor.rs:110 is <=)
+    std::vector<uint8_t> ok(200, 2);
+    const RpcMessage m2(1, MessageType::call(CallBody(1, 1, 1, AuthFlavor::short_(Bytes(ok)), AuthFlavor::none(),
+                                                      Bytes())));
+    CHECK(m2.serialise(c).size() == 4 + 4 + 4 + 16 + 8 + 200 + 8);
+}
+
+// rpc_message.rs:343-367 expected_message_len
+static void test_expected_message_len(Codec&) {
+    const std::vector<uint8_t> raw = fixture("call_auth_unix_16gids_288B");
+    CHECK(expected_message_len(Bytes(raw)) == 288);
+    bool threw = false;
+    try {
+        expected_message_len(Bytes(raw.data(), 3));
+    } catch (const Error& e) {
+        threw = e.code() == ONC_ERR_INCOMPLETE_HEADER;
+    }
+    CHECK(threw);
+    const uint8_t frag[4] = {0, 0, 0, 8};
+    threw = false;
+    try {
+        expected_message_len(Bytes(frag, 4));
+    } catch (const Error& e) {
+        threw = e.code() == ONC_ERR_FRAGMENTED;
+    }
+    CHECK(threw);
+}
+
+// Property test (rpc_message.rs:1134-1153 proptest invariants) over the batch
+// classes: every variant, serialise -> try_from -> equal, lengths agree.
+static void test_batch_round_trip(Codec& c) {
+    uint64_t s = 0x9E3779B97F4A7C15ull;
+    auto rnd = [&]() {
+        s += 0x9E3779B97F4A7C15ull;
+        uint64_t z = s;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return uint32_t((z ^ (z >> 31)) >> 7);
+    };
+    std::vector<std::vector<uint8_t>> store;
+    auto bytes = [&](size_t n) {
+        store.emplace_back(n);
+        for (auto& b : store.back()) b = uint8_t(rnd());
+        return Bytes(store.back());
+    };
+    store.reserve(20000);
+    auto auth = [&]() -> AuthFlavor {
+        switch (rnd() % 5) {
+            case 0: return AuthFlavor::none();
+            case 1: return AuthFlavor::none(bytes(1 + rnd() % 200));
+            case 2: {
+                std::vector<uint32_t> g(rnd() % 17);
+                for (auto& x : g) x = rnd();
+                return AuthFlavor::unix(AuthUnixParams(rnd(), bytes(rnd() % 40), rnd(), rnd(), g));
+            }
+            case 3: return AuthFlavor::short_(bytes(rnd() % 200));
+            default: return AuthFlavor::unknown(3 + rnd() % 1000, bytes(rnd() % 200));
+        }
+    };
+    std::vector<RpcMessage> msgs;
+    BatchEncoder enc;
+    for (int i = 0; i < 3000; ++i) {
+        const uint32_t k = rnd() % 6;
+        if (k < 3) {
+            msgs.emplace_back(rnd(), MessageType::call(CallBody(rnd(), rnd(), rnd(), auth(), auth(), bytes(rnd() % 700))));
+        } else if (k == 3) {
+            AcceptedStatus st = AcceptedStatus::success(bytes(rnd() % 700));
+            const uint32_t w = rnd() % 6;
+            if (w == 2) st = AcceptedStatus::program_mismatch(rnd(), rnd());
+            else if (w) st = AcceptedStatus::of(AcceptedStatus::Kind(w));
+            msgs.emplace_back(rnd(), MessageType::reply(ReplyBody::accepted(AcceptedReply(auth(), st))));
+        } else if (k == 4) {
+            msgs.emplace_back(rnd(), MessageType::reply(ReplyBody::denied(
+                                         RejectedReply::rpc_version_mismatch(rnd(), rnd()))));
+        } else {
+            msgs.emplace_back(rnd(), MessageType::reply(ReplyBody::denied(
+                                         RejectedReply::auth_error(AuthError(rnd() % 8)))));
+        }
+        enc.push(msgs.back());
+    }
+    std::vector<uint8_t> wire;
+    std::vector<uint64_t> off;
+    const std::vector<int32_t> st = enc.serialise_into(c, wire, &off);
+    const std::vector<uint32_t> lens = enc.serialised_lens(c);
+    std::vector<uint32_t> rec_len(msgs.size());
+    for (size_t i = 0; i < msgs.size(); ++i) {
+        CHECK(st[i] == ONC_OK);
+        rec_len[i] = uint32_t(off[i + 1] - off[i]);
+        CHECK(rec_len[i] == lens[i]);
+    }
+    BatchDecoder dec;
+    for (DecodeMode mode : {DecodeMode::Slice, DecodeMode::Bytes}) {
+        const std::vector<Decoded> out = dec.try_from(c, wire.data(), wire.size(), rec_len, mode);
+        for (size_t i = 0; i < msgs.size(); ++i) {
+            CHECK(out[i].ok());
+            CHECK(*out[i].message == msgs[i]);
+        }
+    }
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: %s vectors.json\n", argv[0]);
+        return 2;
+    }
+    std::ifstream f(argv[1]);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    g_json = ss.str();
+    if (g_json.empty()) {
+        std::fprintf(stderr, "cannot read %s\n", argv[1]);
+        return 2;
+    }
+    Codec codec(0);
+    const std::vector<std::pair<const char*, std::function<void(Codec&)>>> tests = {
+        {"test_rpcmessage_auth_unix", test_rpcmessage_auth_unix},
+        {"test_rpcmessage_auth_unix_1gid", test_rpcmessage_auth_unix_1gid},
+        {"test_rpcmessage_reply", test_rpcmessage_reply},
+        {"test_error_vectors", test_error_vectors},
+        {"test_doc_example", test_doc_example},
+        {"test_bench_message_round_trip", test_bench_message_round_trip},
+        {"test_panics", test_panics},
+        {"test_expected_message_len", test_expected_message_len},
+        {"test_batch_round_trip", test_batch_round_trip},
+    };
+    for (const auto& t : tests) {
+        try {
+            t.second(codec);
+            ++g_pass;
+            std::printf("PASS %s\n", t.first);
+        } catch (const std::exception& e) {
+            ++g_fail;
+            std::printf("FAIL %s: %s\n", t.first, e.what());
+        }
+    }
+    std::printf("%d passed, %d failed\n", g_pass, g_fail);
+    return g_fail ? 1 : 0;
+}

@@ -120,6 +120,14 @@ def test_oracle_multithreaded_decode_matches(oracle):
         assert np.array_equal(x.view(np.uint8), y.view(np.uint8))
 
 
+def test_oracle_multithreaded_encode_matches(oracle):
+    hb = S.mixed(3000, seed=11, exotic=0.2)
+    wire, off, st, ln = oracle.encode_batch(hb)
+    out, off2, st2, ln2 = oracle.encode_batch_mt(hb, threads=5)
+    assert out.tobytes()[: len(wire)] == wire
+    assert np.array_equal(off, off2) and np.array_equal(st, st2) and np.array_equal(ln, ln2)
+
+
 def test_shard_bounds_and_bases():
     import onc_rpc_amd.shard as SH
     for n in (0, 1, 7, 1000, 64_000_000):
@@ -130,3 +138,25 @@ def test_shard_bounds_and_bases():
             assert max(h - l for l, h in b) - min(h - l for l, h in b) <= 1
     base, total = SH.exclusive_bases([5, 0, 7, 3])
     assert list(base) == [0, 5, 5, 12] and total == 15
+
+
+def test_expected_message_len_matches_oracle(oracle, golden):
+    """onc_expected_message_len (library host function, rpc_message.rs:343-367)
+    against the oracle on every golden message/error buffer and short prefixes."""
+    import ctypes as C
+    import onc_rpc_amd.runtime as R
+    lib = oracle.load()
+    bufs = [bytes.fromhex(v["hex"]) for sec in ("messages", "errors", "xdrlib", "derived_errors")
+            for v in golden[sec] if "hex" in v]
+    bufs += [b"", b"\x80", b"\x80\x00\x00", b"\x00\x00\x00\x08", b"\xff\xff\xff\xff"]
+    assert len(bufs) > 30
+    for buf in bufs:
+        for cut in {len(buf), min(len(buf), 3), min(len(buf), 4)}:
+            b = buf[:cut]
+            w = C.c_uint32(0)
+            a = np.frombuffer(b + b"\0", np.uint8)
+            want = lib.oracle_expected_message_len(a.ctypes.data, len(b), C.addressof(w))
+            st, got = R.expected_message_len(b)
+            assert st == want, b.hex()
+            if st == 0:
+                assert got == w.value
