@@ -19,22 +19,28 @@
 
 namespace onc {
 
-// Each lane first pulls the first kWinBytes of its record's 16-byte-aligned
-// window into LDS (6 x dwordx4, all issued back to back: one memory latency
-// instead of one per field), laid out [word][lane] so that lanes parsing the
-// same field hit distinct banks. Reads past the window fall back to global.
-constexpr uint32_t kWinWords = 24;
-constexpr uint32_t kWinBytes = 4 * kWinWords;
+// Each lane pulls the start of its record's 16-byte-aligned window into LDS
+// in two rounds of back-to-back dwordx4 loads (one memory latency per round
+// instead of one per field): first kWin1 chunks (64 B: the whole header of an
+// AUTH_NONE call), then, only for records whose header reaches further (the
+// credential length read from the first round), up to kWinChunks chunks
+// (160 B: an AUTH_UNIX call with 16 gids and a 16-byte machine name). The
+// window is laid out [word][lane] so that lanes parsing the same field hit
+// distinct banks. Reads past what was loaded fall back to global loads.
+constexpr uint32_t kWin1 = 4;
+constexpr uint32_t kWinChunks = 10;
+constexpr uint32_t kWinWords = 4 * kWinChunks;
 
 struct Rd {
     uintptr_t base;          // absolute address of record byte 0
     uint32_t q0;             // window offset of record byte 0 (0..15)
+    uint32_t lim;            // window bytes loaded
     const uint32_t* col;     // this lane's window column (stride kTile words)
 
     // Big-endian u32 at record-relative position pos (all 4 bytes valid).
     __device__ __forceinline__ uint32_t be32(uint32_t pos) const {
         const uint32_t q = q0 + pos;
-        if (q + 4u <= kWinBytes) {
+        if (q + 4u <= lim) {
             const uint32_t wi = q >> 2, sh = q & 3u;
             const uint32_t w0 = col[wi * kTile];
             const uint32_t w1 = sh ? col[(wi + 1) * kTile] : 0u;
@@ -58,6 +64,16 @@ struct Rules {
     static constexpr int32_t kShort = MODE == ONC_DECODE_BYTES ? ONC_ERR_INVALID_LENGTH : ONC_ERR_IO_UNEXPECTED_EOF;
 };
 
+// One decoded AUTH_UNIX parameter slot, written with six dwordx4 stores.
+__device__ __forceinline__ void put_unix(onc_unix_params* u, uint32_t stamp, uint32_t uid, uint32_t gid,
+                                         uint32_t ng, uint64_t name_off, uint32_t nl, const uint32_t* gids) {
+    uint4* d = reinterpret_cast<uint4*>(u);
+    d[0] = make_uint4(stamp, uid, gid, ng);
+    d[1] = make_uint4(uint32_t(name_off), uint32_t(name_off >> 32), nl, 0u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[2 + k] = make_uint4(gids[4 * k], gids[4 * k + 1], gids[4 * k + 2], gids[4 * k + 3]);
+}
+
 // Slice mode AuthFlavor::from_cursor (flavor.rs:52-94) with
 // AuthUnixParams::from_cursor (unix_params.rs:90-129) and
 // Opaque::from_wire (opaque.rs:72-98; bound = the whole message, `end`).
@@ -72,7 +88,6 @@ __device__ __forceinline__ int32_t auth_slice(const Rd& R, uint32_t& pos, uint32
         ONC_RD(n);
         if (n > ONC_MAX_AUTH_LEN) return ONC_ERR_INVALID_LENGTH;           // flavor.rs:83-85
         const uint32_t start = pos;
-        onc_unix_params* u = uo + slot;
         uint32_t stamp, nl, uid, gid, ng;
         ONC_RD(stamp);
         ONC_RD(nl);
@@ -84,19 +99,15 @@ __device__ __forceinline__ int32_t auth_slice(const Rd& R, uint32_t& pos, uint32
         ONC_RD(gid);
         ONC_RD(ng);
         if (ng > ONC_MAX_GIDS) return ONC_ERR_INVALID_AUTH_DATA;          // unix_params.rs:112
+        uint32_t gids[ONC_MAX_GIDS];
+#pragma unroll
         for (uint32_t g = 0; g < ONC_MAX_GIDS; ++g) {
             uint32_t v = 0;
             if (g < ng) ONC_RD(v);
-            u->gids[g] = v;
+            gids[g] = v;
         }
         if (pos - start != n) return ONC_ERR_INVALID_AUTH_DATA;          // unix_params.rs:117-119
-        u->stamp = stamp;
-        u->uid = uid;
-        u->gid = gid;
-        u->ngids = ng;
-        u->name_off = rec_off + name_pos;
-        u->name_len = nl;
-        u->reserved = 0;
+        put_unix(uo + slot, stamp, uid, gid, ng, rec_off + name_pos, nl, gids);
         a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
         a.ref = slot;
         return ONC_OK;
@@ -127,7 +138,6 @@ __device__ __forceinline__ int32_t auth_bytes(const Rd& R, uint32_t& pos, uint32
     pos += n + pad4(n);
     a.id = fl;
     if (fl == ONC_AUTH_UNIX) {
-        onc_unix_params* u = uo + slot;
         uint32_t q = bstart;
         uint32_t stamp, nl, uid, gid, ng;
 #define ONC_RDQ(var)                                           \
@@ -146,21 +156,17 @@ __device__ __forceinline__ int32_t auth_bytes(const Rd& R, uint32_t& pos, uint32
         ONC_RDQ(gid);
         ONC_RDQ(ng);
         if (ng > ONC_MAX_GIDS) return ONC_ERR_INVALID_AUTH_DATA;
+        uint32_t gids[ONC_MAX_GIDS];
+#pragma unroll
         for (uint32_t g = 0; g < ONC_MAX_GIDS; ++g) {
             uint32_t v = 0;
             if (g < ng) ONC_RDQ(v);
-            u->gids[g] = v;
+            gids[g] = v;
         }
 #undef ONC_RDQ
         // params.serialised_len() != auth_data.len() -> InvalidAuthData (flavor.rs:204-208)
         if (20u + nl + pad4(nl) + 4u * ng != n) return ONC_ERR_INVALID_AUTH_DATA;
-        u->stamp = stamp;
-        u->uid = uid;
-        u->gid = gid;
-        u->ngids = ng;
-        u->name_off = rec_off + name_pos;
-        u->name_len = nl;
-        u->reserved = 0;
+        put_unix(uo + slot, stamp, uid, gid, ng, rec_off + name_pos, nl, gids);
         a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
         a.ref = slot;
         return ONC_OK;
@@ -282,51 +288,108 @@ __device__ __forceinline__ int32_t parse_record(const Rd& R, uint64_t L, uint64_
 }
 #undef ONC_RD
 
+// decode_kernel: lane per record. The 64-byte descriptors of the
+// workgroup's 256 records are staged in LDS and written out as 16 KiB of
+// contiguous dwordx4 stores (1 KiB per wave instruction, whole 128-byte
+// lines) instead of four scattered 16-byte stores per lane.
 template <int MODE>
 __global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
     __shared__ uint32_t s_win[kWinWords * kTile];
+    static_assert(kWinWords * kTile * 4 >= kTile * sizeof(onc_msg), "descriptor staging reuses the window");
     const int t = threadIdx.x;
-    const uint64_t i = uint64_t(blockIdx.x) * kTile + t;
-    if (i >= a.n) return;
-    const uint64_t b = a.rec_off[i];
-    const uint64_t e = a.rec_off[i + 1];
-    const uint64_t L = e - b;
+    const uint64_t i0 = uint64_t(blockIdx.x) * kTile;
+    const uint64_t i = i0 + t;
+    const bool valid = i < a.n;
+    uint64_t b = 0, L = 0;
+    if (valid) {
+        b = a.rec_off[i];
+        L = a.rec_off[i + 1] - b;
+    }
     const uintptr_t wire = reinterpret_cast<uintptr_t>(a.wire);
     const uintptr_t base = wire + b;
     const uintptr_t win = base & ~uintptr_t(15);
-    // Stage the window: all six 16-byte loads issue back to back; chunks
-    // past the record's last byte re-read its last chunk (never leave the
-    // record's 16-byte-aligned span). Empty records read nothing.
+    const uint32_t q0 = uint32_t(base - win);
+    // Stage the window. Chunks past the record's last byte are not loaded;
+    // empty records read nothing.
+    uint32_t nch = 0;
     if (L != 0) {
-        const uintptr_t last = (wire + e - 1) & ~uintptr_t(15);
-        u32x4 v[kWinWords / 4];
+        const uint32_t avail = uint32_t(min(uint64_t(kWinChunks), (q0 + L + 15) >> 4));
+        nch = min(kWin1, avail);
+        u32x4 v[kWin1];
 #pragma unroll
-        for (uint32_t j = 0; j < kWinWords / 4; ++j) v[j] = gload<u32x4>(min(win + 16 * j, last));
+        for (uint32_t j = 0; j < kWin1; ++j)
+            if (j < nch) v[j] = gload<u32x4>(win + 16 * j);
 #pragma unroll
-        for (uint32_t j = 0; j < kWinWords / 4; ++j) {
-            s_win[(4 * j + 0) * kTile + t] = v[j].x;
-            s_win[(4 * j + 1) * kTile + t] = v[j].y;
-            s_win[(4 * j + 2) * kTile + t] = v[j].z;
-            s_win[(4 * j + 3) * kTile + t] = v[j].w;
+        for (uint32_t j = 0; j < kWin1; ++j) {
+            if (j < nch) {
+                s_win[(4 * j + 0) * kTile + t] = v[j].x;
+                s_win[(4 * j + 1) * kTile + t] = v[j].y;
+                s_win[(4 * j + 2) * kTile + t] = v[j].z;
+                s_win[(4 * j + 3) * kTile + t] = v[j].w;
+            }
+        }
+        // Header extent from the first round: call -> 36 + cred body + verf
+        // flavor/length + 16 bytes of verifier body; reply -> up to 16 bytes
+        // past an accepted verifier.
+        const Rd R1{base, q0, 16 * nch, &s_win[t]};
+        uint32_t need = uint32_t(min(L, uint64_t(16 * kWinChunks)));
+        if (L >= 36 && 16 * nch >= q0 + 36) {
+            const uint32_t mt = R1.be32(8);
+            if (mt == ONC_MSG_CALL) {
+                const uint32_t cl = R1.be32(32);
+                need = cl <= ONC_MAX_AUTH_LEN ? 36 + cl + pad4(cl) + 8 + 16 : 36;
+            } else if (mt == ONC_MSG_REPLY) {
+                const uint32_t vl = R1.be32(20);
+                need = vl <= ONC_MAX_AUTH_LEN ? 24 + vl + pad4(vl) + 16 : 24;
+            }
+        }
+        const uint32_t want = min(avail, (q0 + need + 15) >> 4);
+        if (want > nch) {
+            u32x4 w[kWinChunks - kWin1];
+#pragma unroll
+            for (uint32_t j = kWin1; j < kWinChunks; ++j)
+                if (j < want) w[j - kWin1] = gload<u32x4>(win + 16 * j);
+#pragma unroll
+            for (uint32_t j = kWin1; j < kWinChunks; ++j) {
+                if (j < want) {
+                    s_win[(4 * j + 0) * kTile + t] = w[j - kWin1].x;
+                    s_win[(4 * j + 1) * kTile + t] = w[j - kWin1].y;
+                    s_win[(4 * j + 2) * kTile + t] = w[j - kWin1].z;
+                    s_win[(4 * j + 3) * kTile + t] = w[j - kWin1].w;
+                }
+            }
+            nch = want;
         }
     }
-    const Rd R{base, uint32_t(base - win), &s_win[t]};
+    const Rd R{base, q0, 16 * nch, &s_win[t]};
     onc_msg m;
     uint4* mz = reinterpret_cast<uint4*>(&m);
 #pragma unroll
     for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);
     uint32_t aux0 = 0, aux1 = 0;
-    const int32_t st = parse_record<MODE>(R, L, b, i, m, aux0, aux1, a.out.unix_params);
-    if (st != ONC_OK) {
+    int32_t st = ONC_OK;
+    if (valid) {
+        st = parse_record<MODE>(R, L, b, i, m, aux0, aux1, a.out.unix_params);
+        if (st != ONC_OK) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);
+            for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);
+        }
+        a.out.status[i] = st;
+        a.out.aux0[i] = aux0;
+        a.out.aux1[i] = aux1;
     }
-    uint4* dst = reinterpret_cast<uint4*>(a.out.msgs + i);
+    __syncthreads();                                  // every lane is done with its window
+    uint4* stage = reinterpret_cast<uint4*>(s_win);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) dst[k] = mz[k];
-    a.out.status[i] = st;
-    a.out.aux0[i] = aux0;
-    a.out.aux1[i] = aux1;
+    for (int k = 0; k < 4; ++k) stage[4 * t + k] = mz[k];
+    __syncthreads();
+    const uint64_t nblk = min(uint64_t(kTile), a.n - i0);
+    uint4* dst = reinterpret_cast<uint4*>(a.out.msgs + i0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t j = uint32_t(k * kTile + t);
+        if (j < 4 * nblk) dst[j] = stage[j];
+    }
 }
 
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s) {

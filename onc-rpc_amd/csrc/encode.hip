@@ -88,6 +88,7 @@ __device__ __forceinline__ uint64_t tile_start(const EncArgs& a, uint64_t tile) 
 constexpr int kFastHdrCap = 2048;             // header words per wave tile (8 KiB of LDS)
 constexpr int kFastMapCap = 1024;             // output granules per wave tile
 constexpr int kFastWaves = 4;                 // wave tiles per workgroup
+constexpr int kEmitUnroll = 2;                // output chunks per lane per step
 
 // Per-record LDS entry of enc_emit (two ds_read_b128).
 struct FastEnt {
@@ -124,7 +125,8 @@ struct FastTile {
 //  (a line left partially written costs a read-modify-write at eviction).
 //  Chunks straddling a tile boundary are written with byte stores of only
 //  this tile's bytes, so tiles never exchange data.
-__global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel(EncArgs a) {
+template <int kU>
+__global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) {
     __shared__ FastTile s_tiles[kFastWaves];
 
     const int lane = threadIdx.x & 63;
@@ -193,29 +195,41 @@ __global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel(EncArgs a) {
     const uint64_t E = min(T1, a.out_cap);
     if (E <= T0) return;                              // no bytes (all records failed, or beyond out_cap)
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.msgs);   // >= 64 valid bytes
-    for (uint64_t c = (T0 >> 4) + lane; c < (E + 15) >> 4; c += 64) {
-        const uint64_t o = c << 4;
-        const uint64_t lo = max(o, T0);
-        int r = T.map[(lo >> gs) - G0];
-        FastEnt e = T.ent[r];
-        while (lo >= e.en) e = T.ent[++r];            // sentinel en = T1 > lo
-        uint32_t v[4];
-        if (o >= e.pst && o + 16 <= e.en) {
-            load16_unaligned(e.srcbase + o, v);
-        } else {
-            const int64_t q = (int64_t(o) - int64_t(T0)) >> 2;
+    // kU chunks per lane per step: their loads are all in flight before the
+    // first store (more bytes in flight per wave).
+    const uint64_t cend = (E + 15) >> 4;
+    for (uint64_t c = (T0 >> 4) + lane; c < cend; c += 64 * kU) {
+        uint32_t v[kU][4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint64_t p = o + 4 * i;
-                const bool in_pay = p >= e.pst && p < e.en;
-                const int64_t hidx = q + i + (p >= e.en ? e.dwn : e.dw);
-                const int64_t hcl = hidx < 0 ? 0 : (hidx >= kFastHdrCap ? kFastHdrCap - 1 : hidx);
-                const uint32_t h = T.hdr[hcl];
-                const uint32_t w = gload<uint32_t>(in_pay ? e.srcbase + p : dummy);
-                v[i] = in_pay ? w : h;
+        for (int u = 0; u < kU; ++u) {
+            const uint64_t o = (c + 64 * u) << 4;
+            const uint64_t lo = max(o, T0);
+            if (c + 64 * u >= cend) break;
+            int r = T.map[(lo >> gs) - G0];
+            FastEnt e = T.ent[r];
+            while (lo >= e.en) e = T.ent[++r];            // sentinel en = T1 > lo
+            if (o >= e.pst && o + 16 <= e.en) {
+                load16_unaligned(e.srcbase + o, v[u]);
+            } else {
+                const int64_t q = (int64_t(o) - int64_t(T0)) >> 2;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint64_t p = o + 4 * i;
+                    const bool in_pay = p >= e.pst && p < e.en;
+                    const int64_t hidx = q + i + (p >= e.en ? e.dwn : e.dw);
+                    const int64_t hcl = hidx < 0 ? 0 : (hidx >= kFastHdrCap ? kFastHdrCap - 1 : hidx);
+                    const uint32_t h = T.hdr[hcl];
+                    const uint32_t w = gload<uint32_t>(in_pay ? e.srcbase + p : dummy);
+                    v[u][i] = in_pay ? w : h;
+                }
             }
         }
-        store_chunk(a.out, o, lo, min(o + 16, E), v);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint64_t o = (c + 64 * u) << 4;
+            if (c + 64 * u >= cend) break;
+            store_chunk(a.out, o, max(o, T0), min(o + 16, E), v[u]);
+        }
     }
 }
 
@@ -388,7 +402,7 @@ hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
 
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
     const uint64_t blocks = (num_emit_tiles(a.n) + kFastWaves - 1) / kFastWaves;
-    hipLaunchKernelGGL(enc_emit_kernel, dim3(uint32_t(blocks)), dim3(64 * kFastWaves), 0, s, a);
+    hipLaunchKernelGGL((enc_emit_kernel_t<kEmitUnroll>), dim3(uint32_t(blocks)), dim3(64 * kFastWaves), 0, s, a);
     return hipGetLastError();
 }
 

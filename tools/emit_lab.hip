@@ -288,6 +288,9 @@ int main(int argc, char** argv) {
         {"product_len_scan_emit_fixup", true, [&] { launch_enc_len(a2, 0); launch_scan_tiles(a2.block_sum, a2.block_base, num_tiles(n), 0, d_off + n, 0); launch_enc_emit(a2, 0); launch_enc_fixup(a2, 0); }},
         {"product_scan", false, [&] { launch_scan_tiles(a2.block_sum, a2.block_base, num_tiles(n), 0, d_off + n, 0); }},
         {"product_emit_only", false, [&] { launch_enc_emit(a2, 0); }},
+        {"emit_u1", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<1>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"emit_u2", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"emit_u4", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<4>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
         {"fixup_all_tiles", true, [&] { launch_enc_emit(a2, 0); hipLaunchKernelGGL(flag_all_tiles, dim3(uint32_t((tiles + 255) / 256)), dim3(256), 0, 0, a2.tile_base, tiles); launch_enc_fixup(a2, 0); }},
         {"flag_only", false, [&] { hipLaunchKernelGGL(flag_all_tiles, dim3(uint32_t((tiles + 255) / 256)), dim3(256), 0, 0, a2.tile_base, tiles); }},
         {"copy_256MB_payload_ideal", false,
