@@ -250,7 +250,9 @@ int onc_abi_version(void);
 #define ONC_K_LEN_TILES   4
 #define ONC_K_LEN_APPLY   5
 #define ONC_K_ENC_FIXUP   6
-#define ONC_K_COUNT       7
+#define ONC_K_IOV_LEN     7
+#define ONC_K_IOV_EMIT    8
+#define ONC_K_COUNT       9
 #define ONC_TIMING_ALL    (-1)
 int onc_codec_enable_timing(onc_codec* codec, int enable);
 int onc_codec_kernel_stats(onc_codec* codec, double* ms_total /*[ONC_K_COUNT]*/,
@@ -281,6 +283,32 @@ int onc_encode_lengths(onc_codec* codec, const onc_batch* batch,
 int onc_encode(onc_codec* codec, const onc_batch* batch,
                uint8_t* out, uint64_t out_cap,
                uint64_t* rec_off, int32_t* status, uint32_t* rec_len);
+
+/* Vectored encode (the zero-copy writer the reference
+ * plans in README.md:71-75 and rpc_message.rs:19): only the header part of
+ * every record (everything before the raw payload) is serialised, into
+ * hdr_out[dev] back to back; payloads stay where they are in the batch's
+ * payload arena. Record i on the wire is
+ *     hdr_out[iov[i].hdr_off, +hdr_len) ++ payload_arena[iov[i].payload_off, +payload_len)
+ * and starts at iov[i].wire_off of the equivalent packed send buffer, i.e.
+ * the bytes onc_encode would produce, for a writev()/scatter-gather sender.
+ *   iov[dev, n]    : one entry per record; all zero lengths for a record
+ *                    whose status != ONC_OK.
+ *   status[dev, n] : ONC_OK or ONC_ENC_*; a record whose header would end
+ *                    beyond hdr_cap gets ONC_ENC_WRITE_ZERO and none of its
+ *                    header bytes are written.
+ *   totals[dev, 2] : optional: {header bytes, wire bytes} of the batch. */
+typedef struct onc_iov_rec {
+    uint64_t hdr_off;
+    uint64_t payload_off;
+    uint64_t wire_off;
+    uint32_t hdr_len;
+    uint32_t payload_len;
+} onc_iov_rec;
+
+int onc_encode_iov(onc_codec* codec, const onc_batch* batch,
+                   uint8_t* hdr_out, uint64_t hdr_cap,
+                   onc_iov_rec* iov, int32_t* status, uint64_t* totals);
 
 /* ------------------------------------------------------------------------ */
 /* Decode — RpcMessage::try_from(&[u8]) / try_from(Bytes)                    */

@@ -199,6 +199,8 @@ const char* onc_kernel_name(int k) {
         case ONC_K_LEN_TILES: return "len_tiles_kernel";
         case ONC_K_LEN_APPLY: return "len_apply_kernel";
         case ONC_K_ENC_FIXUP: return "enc_fixup_kernel";
+        case ONC_K_IOV_LEN: return "iov_len_kernel";
+        case ONC_K_IOV_EMIT: return "iov_emit_kernel";
         default: return "?";
     }
 }
@@ -306,6 +308,52 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
     rc = run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
     return run(c, ONC_K_ENC_FIXUP, "enc_fixup", [&] { return onc::launch_enc_fixup(a, c->stream); });
+}
+
+int onc_encode_iov(onc_codec* c, const onc_batch* batch, uint8_t* hdr_out, uint64_t hdr_cap, onc_iov_rec* iov,
+                   int32_t* status, uint64_t* totals) {
+    if (!c || check_batch(batch) != ONC_RC_OK) return ONC_RC_EINVAL;
+    if (batch->n && (!iov || !status || (!hdr_out && hdr_cap))) return ONC_RC_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(hdr_out) & 3) != 0) return ONC_RC_EALIGN;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    if (batch->n == 0) {
+        if (!totals) return ONC_RC_OK;
+        const hipError_t e = hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), c->stream);
+        return e == hipSuccess ? ONC_RC_OK : fail(c, e, "hipMemsetAsync");
+    }
+    const uint64_t tiles = onc::num_emit_tiles(batch->n);
+    int rc = ensure_scratch(c, tiles);
+    if (rc != ONC_RC_OK) return rc;
+    const uint64_t T = c->scratch_tiles;
+    const uint64_t B = T / 4 + 1;
+    onc::IovArgs a{};
+    a.n = batch->n;
+    a.msgs = batch->msgs;
+    a.unix = batch->unix_params;
+    a.auth_arena = batch->auth_arena;
+    a.payload_arena = batch->payload_arena;
+    a.hdr_out = hdr_out;
+    a.hdr_cap = hdr_out ? hdr_cap : 0;
+    a.iov = iov;
+    a.status = status;
+    a.totals = totals;
+    a.tile_sum = c->scratch;
+    a.block_len = c->scratch + 3 * T;
+    a.block_len_base = c->scratch + 3 * T + B;
+    a.block_hdr = c->scratch + 2 * T;
+    a.block_hdr_base = c->scratch + 2 * T + B;
+    const uint64_t nblk = onc::num_tiles(batch->n);
+    rc = run(c, ONC_K_IOV_LEN, "iov_len", [&] { return onc::launch_iov_len(a, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
+        return onc::launch_scan_tiles(a.block_len, a.block_len_base, nblk, 0, nullptr, c->stream);
+    });
+    if (rc != ONC_RC_OK) return rc;
+    rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
+        return onc::launch_scan_tiles(a.block_hdr, a.block_hdr_base, nblk, 0, nullptr, c->stream);
+    });
+    if (rc != ONC_RC_OK) return rc;
+    return run(c, ONC_K_IOV_EMIT, "iov_emit", [&] { return onc::launch_iov_emit(a, c->stream); });
 }
 
 int onc_decode(onc_codec* c, const uint8_t* wire, const uint64_t* rec_off, uint64_t n, int mode,

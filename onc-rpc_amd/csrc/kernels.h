@@ -27,6 +27,24 @@ struct EncArgs {
     uint64_t* block_base;   // exclusive scan of block_sum
 };
 
+struct IovArgs {
+    uint64_t n;
+    const onc_msg* msgs;
+    const onc_unix_params* unix;
+    const uint8_t* auth_arena;
+    const uint8_t* payload_arena;
+    uint8_t* hdr_out;
+    uint64_t hdr_cap;
+    onc_iov_rec* iov;
+    int32_t* status;
+    uint64_t* totals;          // optional [2]
+    uint64_t* tile_sum;        // per 64 records: (wire bytes << 16) | header bytes
+    uint64_t* block_len;       // per 256 records
+    uint64_t* block_hdr;
+    uint64_t* block_len_base;  // exclusive scans
+    uint64_t* block_hdr_base;
+};
+
 struct DecArgs {
     uint64_t n;
     const uint8_t* wire;
@@ -38,6 +56,9 @@ struct DecArgs {
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s);
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s);
 hipError_t launch_enc_fixup(const EncArgs& a, hipStream_t s);
+// iov.hip
+hipError_t launch_iov_len(const IovArgs& a, hipStream_t s);
+hipError_t launch_iov_emit(const IovArgs& a, hipStream_t s);
 // scan.hip
 hipError_t launch_scan_tiles(const uint64_t* in, uint64_t* out_excl, uint64_t count, uint64_t base,
                              uint64_t* total_out, hipStream_t s);

@@ -63,7 +63,13 @@ UNIX_DTYPE = np.dtype({
     "offsets": [0, 4, 8, 12, 16, 24, 28, 32],
     "itemsize": 96,
 })
-assert MSG_DTYPE.itemsize == 64 and UNIX_DTYPE.itemsize == 96
+IOV_DTYPE = np.dtype({
+    "names": ["hdr_off", "payload_off", "wire_off", "hdr_len", "payload_len"],
+    "formats": ["<u8", "<u8", "<u8", "<u4", "<u4"],
+    "offsets": [0, 8, 16, 24, 28],
+    "itemsize": 32,
+})
+assert MSG_DTYPE.itemsize == 64 and UNIX_DTYPE.itemsize == 96 and IOV_DTYPE.itemsize == 32
 
 
 def pack_kind_len(kind, length):

@@ -18,8 +18,9 @@ _LIB = None
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libonc_rpc_amd.so")
 
 K_NAMES = ["enc_len_kernel", "scan_tiles_kernel", "enc_emit_kernel", "decode_kernel",
-           "len_tiles_kernel", "len_apply_kernel", "enc_fixup_kernel"]
-K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY, K_ENC_FIXUP = range(7)
+           "len_tiles_kernel", "len_apply_kernel", "enc_fixup_kernel", "iov_len_kernel", "iov_emit_kernel"]
+(K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY, K_ENC_FIXUP, K_IOV_LEN,
+ K_IOV_EMIT) = range(9)
 K_COUNT = len(K_NAMES)
 
 # every symbol include/onc_rpc.h declares
@@ -28,7 +29,7 @@ EXPORTED = [
     "onc_codec_sync", "onc_codec_reserve", "onc_codec_last_error", "onc_status_str",
     "onc_codec_enable_timing", "onc_codec_kernel_stats", "onc_codec_reset_stats",
     "onc_kernel_name", "onc_encode_lengths", "onc_encode", "onc_decode", "onc_scan_lengths",
-    "onc_expected_message_len",
+    "onc_expected_message_len", "onc_encode_iov",
 ]
 
 
@@ -74,6 +75,7 @@ def load_library(path=LIB_PATH):
     lib.onc_encode.argtypes = [vp, C.POINTER(OncBatch), vp, u64, vp, vp, vp]
     lib.onc_decode.argtypes = [vp, vp, vp, u64, i32, C.POINTER(OncDecoded)]
     lib.onc_scan_lengths.argtypes = [vp, vp, u64, u64, vp]
+    lib.onc_encode_iov.argtypes = [vp, C.POINTER(OncBatch), vp, u64, vp, vp, vp]
     lib.onc_expected_message_len.argtypes = [C.c_char_p, u64, C.POINTER(C.c_uint32)]
     lib.onc_expected_message_len.restype = C.c_int32
     for name in EXPORTED:
@@ -198,6 +200,13 @@ class Codec:
         cap = out.numel() if out_cap is None else out_cap
         self._check(self.lib.onc_encode(self.h, C.byref(b), _ptr(out), cap, _ptr(rec_off), _ptr(status),
                                         _ptr(rec_len)), "onc_encode")
+
+    def encode_iov(self, batch: DeviceBatch, hdr_out, iov, status, totals=None, hdr_cap=None):
+        """Vectored encode: headers into hdr_out, one onc_iov_rec (32 B) per record in iov."""
+        b = batch.c_struct()
+        cap = hdr_out.numel() if hdr_cap is None else hdr_cap
+        self._check(self.lib.onc_encode_iov(self.h, C.byref(b), _ptr(hdr_out), cap, _ptr(iov), _ptr(status),
+                                            _ptr(totals)), "onc_encode_iov")
 
     # -- decode -----------------------------------------------------------
     def decode(self, wire, rec_off, n, mode, msgs, unix, status, aux0, aux1):

@@ -312,3 +312,73 @@ def test_full_size_config1_loopback(codec, R, oracle):
     sub = L.HostBatch(hb.msgs[lo:hi].copy(), hb.unix, hb.auth_arena, hb.payload_arena)
     o_wire = oracle.encode_batch(sub)[0]
     assert out[lo * 300:hi * 300].cpu().numpy().tobytes() == o_wire
+
+
+# ---------------------------------------------------------------------------
+# Vectored encode: headers + in-place payload slices.
+def iov_wire(hb, hdr, iov, st):
+    """Reassemble the packed wire from an iov encode (what writev would send)."""
+    parts = []
+    for i in range(len(iov)):
+        if st[i] != 0:
+            continue
+        h = iov[i]
+        parts.append(hdr[int(h["hdr_off"]):int(h["hdr_off"]) + int(h["hdr_len"])].tobytes())
+        po = int(h["payload_off"])
+        parts.append(hb.payload_arena[po:po + int(h["payload_len"])].tobytes())
+    return b"".join(parts)
+
+
+def gpu_iov(R, codec, hb, hdr_cap=None):
+    import torch
+    db = R.DeviceBatch.from_host(hb, "cuda")
+    n = hb.n
+    lens = R.codec_lengths(codec, db)
+    cap = int(lens.sum()) if hdr_cap is None else hdr_cap
+    hdr = torch.zeros(max(16, cap + 16), dtype=torch.uint8, device="cuda")
+    iov = torch.zeros(max(1, n) * 32, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(max(1, n), dtype=torch.int32, device="cuda")
+    tot = torch.zeros(2, dtype=torch.int64, device="cuda")
+    codec.encode_iov(db, hdr, iov, st, tot, hdr_cap=cap)
+    codec.sync()
+    return (hdr.cpu().numpy(), iov.cpu().numpy().view(L.IOV_DTYPE)[:n], st.cpu().numpy()[:n],
+            tot.cpu().numpy().view(np.uint64))
+
+
+@pytest.mark.parametrize("gen", ["call_none", "call_unix16", "mixed_exotic", "random"])
+def test_iov_encode_matches_packed_encode(codec, R, oracle, gen):
+    hb = {"call_none": lambda: S.call_none(3000, 256),
+          "call_unix16": lambda: S.call_unix16(2000, 1024),
+          "mixed_exotic": lambda: S.mixed(3000, seed=5, pmin=0, pmax=500, exotic=0.3),
+          "random": lambda: L.build_batch(S.random_messages(1500, seed=77))}[gen]()
+    o_wire, o_off, o_st, _ = oracle.encode_batch(hb)
+    hdr, iov, st, tot = gpu_iov(R, codec, hb)
+    assert np.array_equal(st, o_st)
+    ok = st == 0
+    assert np.array_equal(iov["wire_off"][ok], o_off[:-1][ok])
+    assert iov_wire(hb, hdr, iov, st) == o_wire
+    assert int(tot[1]) == len(o_wire)
+    assert int(tot[0]) == int(iov["hdr_len"].sum())
+    # headers are packed back to back
+    hl = iov["hdr_len"].astype(np.uint64)
+    assert np.array_equal(iov["hdr_off"][ok], (np.cumsum(hl) - hl)[ok])
+    assert not iov["hdr_len"][~ok].any() and not iov["payload_len"][~ok].any()
+
+
+def test_iov_encode_header_capacity(codec, R, oracle):
+    hb = S.mixed(700, seed=12, pmin=0, pmax=100)
+    full_hdr, full_iov, full_st, _ = gpu_iov(R, codec, hb)
+    total = int(full_iov["hdr_len"].sum())
+    for cap in (0, 37, total // 2, total - 1):
+        hdr, iov, st, _ = gpu_iov(R, codec, hb, hdr_cap=cap)
+        ends = full_iov["hdr_off"] + full_iov["hdr_len"]
+        want = np.where((full_st == 0) & (ends > cap), 105, full_st)
+        assert np.array_equal(st, want), cap
+        fit = (full_st == 0) & (ends <= cap)
+        # every record that fits has its header bytes written
+        for i in np.nonzero(fit)[0][:200]:
+            a, b = int(full_iov["hdr_off"][i]), int(ends[i])
+            assert hdr[a:b].tobytes() == full_hdr[a:b].tobytes()
+        # nothing past the last fitting header is written
+        lim = int(ends[fit].max()) if fit.any() else 0
+        assert not hdr[lim:cap].any()

@@ -56,6 +56,8 @@ int main(void){
  printf("%zu %zu %zu %zu %zu\n", offsetof(onc_msg,msg_type), offsetof(onc_msg,u), offsetof(onc_msg,payload_len),
         offsetof(onc_msg,payload_off), offsetof(onc_msg,cred));
  printf("%zu %zu %zu\n", offsetof(onc_msg,verf), offsetof(onc_unix_params,name_off), offsetof(onc_unix_params,gids));
+ printf("%zu %zu %zu %zu %zu\n", sizeof(onc_iov_rec), offsetof(onc_iov_rec,payload_off), offsetof(onc_iov_rec,wire_off),
+        offsetof(onc_iov_rec,hdr_len), offsetof(onc_iov_rec,payload_len));
  return 0;}
 '''
     with tempfile.TemporaryDirectory() as d:
@@ -68,7 +70,9 @@ int main(void){
     f = L.MSG_DTYPE.fields
     assert vals[3:8] == [f["msg_type"][1], f["f0"][1], f["payload_len"][1], f["payload_off"][1], f["cred_id"][1]]
     u = L.UNIX_DTYPE.fields
-    assert vals[8:] == [f["verf_id"][1], u["name_off"][1], u["gids"][1]]
+    assert vals[8:11] == [f["verf_id"][1], u["name_off"][1], u["gids"][1]]
+    v = L.IOV_DTYPE.fields
+    assert vals[11:] == [32, v["payload_off"][1], v["wire_off"][1], v["hdr_len"][1], v["payload_len"][1]]
 
 
 def test_build_describe_round_trip():
