@@ -252,7 +252,9 @@ int onc_abi_version(void);
 #define ONC_K_ENC_FIXUP   6
 #define ONC_K_IOV_LEN     7
 #define ONC_K_IOV_EMIT    8
-#define ONC_K_COUNT       9
+#define ONC_K_FRAME       9
+#define ONC_K_FRAME_WRITE 10
+#define ONC_K_COUNT       11
 #define ONC_TIMING_ALL    (-1)
 int onc_codec_enable_timing(onc_codec* codec, int enable);
 int onc_codec_kernel_stats(onc_codec* codec, double* ms_total /*[ONC_K_COUNT]*/,
@@ -326,6 +328,25 @@ int onc_decode(onc_codec* codec, const uint8_t* wire, const uint64_t* rec_off,
  * bit clear). Host memory, synchronous; the framing helper a caller uses to
  * cut one message out of a socket buffer. */
 int32_t onc_expected_message_len(const uint8_t* data, uint64_t len, uint32_t* out);
+
+/* Framing of a stream buffer of back-to-back record-marked messages (a
+ * socket read buffer): the caller's loop of expected_message_len
+ * (src/rpc_message.rs:343-367) + one-message slices
+ * (rpc_message.rs:238-242), in parallel on the device with the same result.
+ * From offset 0, records are framed while the remaining bytes hold a whole
+ * record and fewer than max_records were framed.
+ *   rec_off[dev, max_records + 1]: starts of the framed records, then the
+ *                     end of the last one (= bytes consumed).
+ *   result[dev, 5]  : {n, consumed, status, aux0, aux1}; status is ONC_OK when
+ *                     the buffer ends on a record boundary or max_records
+ *                     were framed, else why the next record cannot be cut:
+ *                     ONC_ERR_INCOMPLETE_HEADER (< 4 bytes left),
+ *                     ONC_ERR_FRAGMENTED (last-fragment bit clear) or
+ *                     ONC_ERR_INCOMPLETE_MESSAGE {aux0 = bytes left,
+ *                     aux1 = record length} (wait for more data).
+ * SURVEY §8(f) rank 1. */
+int onc_frame_stream(onc_codec* codec, const uint8_t* wire, uint64_t len,
+                     uint64_t* rec_off, uint64_t max_records, uint64_t* result);
 
 /* Exclusive scan of record lengths into offsets:
  * rec_off[0] = base, rec_off[i+1] = rec_off[i] + rec_len[i]  ([dev]). */

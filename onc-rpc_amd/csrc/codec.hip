@@ -18,6 +18,8 @@ struct onc_codec {
     // scratch (u64 words): [tile_sum | tile_base | block_sum | block_base]
     uint64_t* scratch = nullptr;
     uint64_t scratch_tiles = 0;
+    uint8_t* frame_scratch = nullptr;   // onc_frame_stream per-chunk state
+    uint64_t frame_chunks = 0;
     uint32_t timing = 0;   // bitmask of ONC_K_* ids whose launches are bracketed
     struct Pending {
         int kernel;
@@ -138,6 +140,7 @@ int onc_codec_destroy(onc_codec* c) {
     }
     for (auto e : c->spare) (void)hipEventDestroy(e);
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->frame_scratch) (void)hipFree(c->frame_scratch);
     delete c;
     return ONC_RC_OK;
 }
@@ -201,6 +204,8 @@ const char* onc_kernel_name(int k) {
         case ONC_K_ENC_FIXUP: return "enc_fixup_kernel";
         case ONC_K_IOV_LEN: return "iov_len_kernel";
         case ONC_K_IOV_EMIT: return "iov_emit_kernel";
+        case ONC_K_FRAME: return "frame_chunks_kernel";
+        case ONC_K_FRAME_WRITE: return "frame_write_kernel";
         default: return "?";
     }
 }
@@ -354,6 +359,67 @@ int onc_encode_iov(onc_codec* c, const onc_batch* batch, uint8_t* hdr_out, uint6
     });
     if (rc != ONC_RC_OK) return rc;
     return run(c, ONC_K_IOV_EMIT, "iov_emit", [&] { return onc::launch_iov_emit(a, c->stream); });
+}
+
+// Per-chunk framing state: 56 bytes per chunk + the count scan's tile sums.
+static size_t frame_bytes(uint64_t P) { return P * 56 + (onc::num_tiles(P) + 1) * 16 + 64; }
+
+int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* rec_off, uint64_t max_records,
+                     uint64_t* result) {
+    if (!c || !rec_off || !result || (len && !wire)) return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    hipError_t e = hipMemsetAsync(result, 0, 5 * sizeof(uint64_t), c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
+    if (e != hipSuccess) return fail(c, e, "hipMemsetAsync");
+    if (len == 0 || max_records == 0) return ONC_RC_OK;   // nothing framed, nothing consumed
+    const uint64_t P = (len + onc::kFrameChunk - 1) / onc::kFrameChunk;
+    if (P > c->frame_chunks) {
+        uint64_t want = c->frame_chunks ? c->frame_chunks : 4096;
+        while (want < P) want *= 2;
+        if (c->frame_scratch) {
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipFree(c->frame_scratch);
+            c->frame_scratch = nullptr;
+            c->frame_chunks = 0;
+        }
+        e = hipMalloc(&c->frame_scratch, frame_bytes(want));
+        if (e != hipSuccess) return fail(c, e, "hipMalloc(frame scratch)");
+        c->frame_chunks = want;
+    }
+    const uint64_t Q = c->frame_chunks;
+    uint8_t* f = c->frame_scratch;
+    onc::FrameArgs a{};
+    a.wire = wire;
+    a.len = len;
+    a.nchunks = P;
+    a.max_records = max_records;
+    a.rec_off = rec_off;
+    a.result = result;
+    a.g = reinterpret_cast<uint64_t*>(f);
+    a.x = reinterpret_cast<uint64_t*>(f + 8 * Q);
+    a.cnt_base = reinterpret_cast<uint64_t*>(f + 16 * Q);
+    a.aux = reinterpret_cast<uint32_t*>(f + 24 * Q);
+    a.cnt = reinterpret_cast<uint32_t*>(f + 32 * Q);
+    a.st = reinterpret_cast<int32_t*>(f + 36 * Q);
+    a.cnt_eff = reinterpret_cast<uint32_t*>(f + 40 * Q);
+    a.fail = f + 44 * Q;
+    uint64_t* tail = reinterpret_cast<uint64_t*>(f + 56 * Q);
+    const uint64_t nt = onc::num_tiles(P);
+    uint64_t* tile_sum = tail;
+    uint64_t* tile_base = tail + nt + 1;
+    a.first_fail = tail + 2 * (nt + 1);
+    a.first_stop = a.first_fail + 1;
+    int rc = run(c, ONC_K_FRAME, "frame_chunks", [&] { return onc::launch_frame_chunks(a, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    rc = run(c, ONC_K_LEN_TILES, "len_tiles", [&] { return onc::launch_len_tiles(a.cnt_eff, P, tile_sum, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    rc = run(c, ONC_K_SCAN_TILES, "scan_tiles",
+             [&] { return onc::launch_scan_tiles(tile_sum, tile_base, nt, 0, nullptr, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    rc = run(c, ONC_K_LEN_APPLY, "len_apply",
+             [&] { return onc::launch_len_apply(a.cnt_eff, P, tile_base, a.cnt_base, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    return run(c, ONC_K_FRAME_WRITE, "frame_write", [&] { return onc::launch_frame_write(a, c->stream); });
 }
 
 int onc_decode(onc_codec* c, const uint8_t* wire, const uint64_t* rec_off, uint64_t n, int mode,

@@ -1,0 +1,287 @@
+// frame.hip — record framing of a byte stream on gfx950.
+//
+// The reference frames one message at a time: the caller runs
+// expected_message_len (src/rpc_message.rs:343-367) on the remaining bytes
+// and cuts a one-message slice of that length (the contract of every
+// TryFrom<&[u8]>, rpc_message.rs:238-242). Record k+1's start depends on
+// record k's header: a serial chain. Here it is framed in parallel by
+// speculation + verification, with the same result as the serial loop:
+//
+//   frame_chunks  lane per 1 KiB chunk: guess the first record start in the
+//                 chunk (the first position that looks like an ONC-RPC
+//                 header: last-fragment bit, length within the buffer,
+//                 message type 0 with rpcvers 2 or 1 with reply_stat 0/1),
+//                 then follow the exact chain (header length only, as the
+//                 reference does) out of the chunk: exit position and record
+//                 count, or where and why the chain stops. Chunk 0 starts
+//                 at byte 0.
+//   frame_verify  lane per chunk: a guessed chunk is consistent when its
+//                 chain lands exactly on the guess of the chunk it lands in
+//                 and every chunk it jumps over has no guess. Because chunk 0
+//                 is exact, every guessed chunk before the first
+//                 inconsistency is on the true chain (induction).
+//   frame_walk    one wave, only when a check failed (payload bytes that
+//                 look like headers, or records that do not look like
+//                 RPC messages): walks the true chain from the first
+//                 failure, re-chasing chunks whose guess was wrong, skipping
+//                 verified stretches with 64-wide ballots.
+//   counts -> scan (len_tiles/scan_tiles/len_apply) -> frame_write: every
+//                 chunk on the chain re-chases its records writing rec_off.
+#include "common.h"
+#include "kernels.h"
+
+namespace onc {
+
+constexpr uint64_t kNone = ~0ull;
+constexpr int32_t kExit = -1;   // st: the chain left the chunk at x (more records follow)
+// st >= 0: the chain ends in this chunk: ONC_OK (the buffer ends exactly at
+// x), or the expected_message_len error / IncompleteMessage at position x.
+
+__device__ __forceinline__ uint32_t be_at(uintptr_t base, uint64_t p) { return bswap(load4(base + p)); }
+
+struct Chase {
+    uint64_t x;
+    uint32_t cnt;      // records started before leaving [p, lim)
+    int32_t st;
+    uint32_t aux0, aux1;
+};
+
+// The caller's loop from record start p while p < lim.
+__device__ __forceinline__ Chase chase(const FrameArgs& a, uint64_t p, uint64_t lim) {
+    const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
+    Chase c{p, 0, kExit, 0, 0};
+    while (p < lim) {
+        if (a.len - p < 4) {                       // expected_message_len: rpc_message.rs:344-346
+            c.st = ONC_ERR_INCOMPLETE_HEADER;
+            break;
+        }
+        const uint32_t h = be_at(base, p);
+        if ((h & 0x80000000u) == 0) {              // :359-362
+            c.st = ONC_ERR_FRAGMENTED;
+            break;
+        }
+        const uint64_t want = uint64_t(h & 0x7FFFFFFFu) + 4;
+        if (a.len - p < want) {                    // the one-message slice would be short
+            c.st = ONC_ERR_INCOMPLETE_MESSAGE;
+            c.aux0 = uint32_t(a.len - p);
+            c.aux1 = uint32_t(want);
+            break;
+        }
+        ++c.cnt;
+        p += want;
+    }
+    if (c.st == kExit && p >= a.len) c.st = ONC_OK;   // the last record ends the buffer
+    c.x = p;
+    return c;
+}
+
+// First position in [c0, c1) whose bytes look like a record start (a guess:
+// correctness never depends on it). 64 positions per step from an 80-byte
+// register window of five aligned 16-byte loads.
+__device__ __forceinline__ uint64_t guess_start(const FrameArgs& a, uint64_t c0, uint64_t c1) {
+    const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
+    const uint64_t lastblk = (a.len - 1) & ~uint64_t(15);   // last 16-byte block holding a buffer byte
+    for (uint64_t blk = c0 & ~uint64_t(15); blk < c1; blk += 64) {
+        uint32_t w[20];
+#pragma unroll
+        for (int b = 0; b < 5; ++b) {
+            const uint64_t o = blk + 16 * b;
+            const u32x4 v = gload<u32x4>(base + (o <= lastblk ? o : lastblk));
+            w[4 * b] = v.x;
+            w[4 * b + 1] = v.y;
+            w[4 * b + 2] = v.z;
+            w[4 * b + 3] = v.w;
+        }
+        uint64_t hit = 0;
+#pragma unroll
+        for (int k = 0; k < 64; ++k) {
+            const uint64_t p = blk + k;
+            const uint32_t sh = k & 3;
+            const int wi = k >> 2;
+            const uint32_t h = bswap(funnel(w[wi], w[wi + 1], sh));
+            const uint32_t mt = bswap(funnel(w[wi + 2], w[wi + 3], sh));
+            const uint32_t rv = bswap(funnel(w[wi + 3], w[wi + 4], sh));
+            const uint64_t want = uint64_t(h & 0x7FFFFFFFu) + 4;
+            const bool plausible = (h & 0x80000000u) && want >= 24 && p + 16 <= a.len && want <= a.len - p &&
+                                   (mt == 0 ? rv == 2u : (mt == 1 && rv <= 1u)) && p >= c0 && p < c1;
+            hit |= uint64_t(plausible) << k;
+        }
+        if (hit) return blk + __ffsll(static_cast<unsigned long long>(hit)) - 1;
+    }
+    return kNone;
+}
+
+__device__ __forceinline__ void put_chase(const FrameArgs& a, uint64_t t, const Chase& c) {
+    a.x[t] = c.x;
+    a.cnt[t] = c.cnt;
+    a.st[t] = c.st;
+    a.aux[2 * t] = c.aux0;
+    a.aux[2 * t + 1] = c.aux1;
+}
+
+__global__ __launch_bounds__(256) void frame_chunks_kernel(FrameArgs a) {
+    const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        *a.first_fail = kNone;
+        *a.first_stop = kNone;
+    }
+    if (t >= a.nchunks) return;
+    const uint64_t c0 = t * kFrameChunk;
+    const uint64_t c1 = min(c0 + kFrameChunk, a.len);
+    const uint64_t g = t == 0 ? 0 : guess_start(a, c0, c1);   // chunk 0 starts at byte 0
+    a.g[t] = g;
+    if (g == kNone) {
+        put_chase(a, t, Chase{kNone, 0, kExit, 0, 0});
+        return;
+    }
+    put_chase(a, t, chase(a, g, c1));
+}
+
+// fail[t] = 1 when guessed chunk t's chain does not land on a guess, or jumps
+// over a guessed chunk; first_stop = first guessed chunk whose chain ends.
+__global__ __launch_bounds__(256) void frame_verify_kernel(FrameArgs a) {
+    const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= a.nchunks) return;
+    uint8_t bad = 0;
+    const uint64_t g = a.g[t];
+    if (g != kNone) {
+        if (a.st[t] == kExit) {
+            const uint64_t x = a.x[t];
+            const uint64_t j = x / kFrameChunk;
+            if (j >= a.nchunks || a.g[j] != x) bad = 1;
+            for (uint64_t k = t + 1; k < j && !bad; ++k)
+                if (a.g[k] != kNone) bad = 1;
+        } else {
+            atomicMin(reinterpret_cast<unsigned long long*>(a.first_stop), static_cast<unsigned long long>(t));
+        }
+    }
+    a.fail[t] = bad;
+    if (bad) atomicMin(reinterpret_cast<unsigned long long*>(a.first_fail), static_cast<unsigned long long>(t));
+}
+
+// First k in [t, lim) with pred(k), scanning 64 chunks per step (all lanes
+// of the wave call it with the same arguments); lim if none.
+template <class P>
+__device__ __forceinline__ uint64_t wave_find(uint64_t t, uint64_t lim, P pred) {
+    const int lane = threadIdx.x & 63;
+    for (uint64_t b = t; b < lim; b += 64) {
+        const uint64_t k = b + lane;
+        const uint64_t m = __ballot(k < lim && pred(k));
+        if (m) return b + __ffsll(static_cast<unsigned long long>(m)) - 1;
+    }
+    return lim;
+}
+
+// One wave. No-op when every guess was verified, or when the true chain
+// ends (first_stop) before the first failure. Otherwise the first failing
+// chunk is on the true chain; walk from there. At a chain chunk t with true
+// entry E: if g[t] == E and its check passed, the chain is verified up to
+// the next failing chunk (which is then on the chain, unless the chain
+// stops first); else re-chase t from E and step to the chunk its chain lands
+// in, clearing the guesses of chunks the record jumps over.
+__global__ __launch_bounds__(64) void frame_walk_kernel(FrameArgs a) {
+    const int lane = threadIdx.x;
+    const uint64_t f0 = *a.first_fail;
+    if (f0 == kNone) return;
+    const uint64_t s0 = *a.first_stop;
+    if (s0 != kNone && s0 < f0) return;
+    const uint64_t P = a.nchunks;
+    uint64_t t = f0, E = a.g[f0];
+    for (;;) {
+        const uint64_t g = a.g[t];
+        if (g == E && a.fail[t] == 0) {
+            const uint64_t f2 = wave_find(t + 1, P, [&](uint64_t k) { return a.fail[k] != 0; });
+            const uint64_t s2 =
+                wave_find(t, f2, [&](uint64_t k) { return a.g[k] != kNone && a.st[k] != kExit; });
+            if (s2 < f2 || f2 >= P) {
+                if (lane == 0) *a.first_stop = s2 < f2 ? s2 : kNone;
+                break;
+            }
+            t = f2;
+            E = a.g[f2];
+            continue;
+        }
+        Chase c;
+        if (g != E) {
+            c = chase(a, E, min((t + 1) * kFrameChunk, a.len));   // same in every lane
+            if (lane == 0) {
+                a.g[t] = E;
+                put_chase(a, t, c);
+            }
+            __threadfence();
+        } else {
+            c = Chase{a.x[t], a.cnt[t], a.st[t], a.aux[2 * t], a.aux[2 * t + 1]};
+        }
+        if (c.st != kExit) {
+            if (lane == 0) *a.first_stop = t;
+            break;
+        }
+        const uint64_t j = c.x / kFrameChunk;
+        for (uint64_t k = t + 1 + lane; k < j; k += 64) a.g[k] = kNone;
+        __threadfence();
+        t = j;
+        E = c.x;
+    }
+}
+
+// Records of chunk t that belong to the framed stream.
+__global__ __launch_bounds__(256) void frame_counts_kernel(FrameArgs a) {
+    const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= a.nchunks) return;
+    const uint64_t s = *a.first_stop;
+    a.cnt_eff[t] = (a.g[t] != kNone && t <= s) ? a.cnt[t] : 0u;
+}
+
+__device__ __forceinline__ void put_result(const FrameArgs& a, uint64_t n, uint64_t consumed, int32_t st,
+                                           uint32_t aux0, uint32_t aux1) {
+    a.rec_off[n] = consumed;
+    a.result[0] = n;
+    a.result[1] = consumed;
+    a.result[2] = uint64_t(int64_t(st));
+    a.result[3] = aux0;
+    a.result[4] = aux1;
+}
+
+__global__ __launch_bounds__(256) void frame_write_kernel(FrameArgs a) {
+    const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= a.nchunks) return;
+    const uint32_t ce = a.cnt_eff[t];
+    const uint64_t k0 = a.cnt_base[t];
+    if (ce != 0 && k0 <= a.max_records) {
+        const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
+        uint64_t p = a.g[t];
+        for (uint32_t i = 0; i < ce; ++i) {
+            const uint64_t k = k0 + i;
+            if (k == a.max_records) {
+                // capacity: record max_records is not framed; stop before it
+                put_result(a, k, p, ONC_OK, 0, 0);
+                break;
+            }
+            a.rec_off[k] = p;
+            p += uint64_t(be_at(base, p) & 0x7FFFFFFFu) + 4;
+        }
+    }
+    if (t == *a.first_stop) {
+        const uint64_t n = k0 + ce;
+        // reaching max_records ends the caller's loop before it looks further
+        if (n < a.max_records) put_result(a, n, a.x[t], a.st[t], a.aux[2 * t], a.aux[2 * t + 1]);
+        else if (n == a.max_records) put_result(a, n, a.x[t], ONC_OK, 0, 0);
+    }
+}
+
+hipError_t launch_frame_chunks(const FrameArgs& a, hipStream_t s) {
+    const uint32_t blocks = uint32_t((a.nchunks + 255) / 256);
+    hipLaunchKernelGGL(frame_chunks_kernel, dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(frame_verify_kernel, dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(frame_walk_kernel, dim3(1), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(frame_counts_kernel, dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_write(const FrameArgs& a, hipStream_t s) {
+    const uint32_t blocks = uint32_t((a.nchunks + 255) / 256);
+    hipLaunchKernelGGL(frame_write_kernel, dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace onc

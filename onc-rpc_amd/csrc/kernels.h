@@ -45,6 +45,28 @@ struct IovArgs {
     uint64_t* block_hdr_base;
 };
 
+constexpr uint64_t kFrameChunk = 1024;   // stream bytes per framing lane
+
+struct FrameArgs {
+    const uint8_t* wire;
+    uint64_t len;
+    uint64_t nchunks;
+    uint64_t max_records;
+    uint64_t* rec_off;      // max_records + 1
+    uint64_t* result;       // [5] n, consumed, status, aux0, aux1
+    // per chunk
+    uint64_t* g;            // guessed / verified first record start (~0 = none)
+    uint64_t* x;            // exit or stop position of the chain
+    uint32_t* cnt;          // records started in the chunk
+    int32_t* st;            // -1 = left the chunk, else the stop status
+    uint32_t* aux;          // 2 per chunk
+    uint8_t* fail;
+    uint32_t* cnt_eff;      // records framed from this chunk
+    uint64_t* cnt_base;     // exclusive scan of cnt_eff
+    uint64_t* first_fail;
+    uint64_t* first_stop;
+};
+
 struct DecArgs {
     uint64_t n;
     const uint8_t* wire;
@@ -59,6 +81,9 @@ hipError_t launch_enc_fixup(const EncArgs& a, hipStream_t s);
 // iov.hip
 hipError_t launch_iov_len(const IovArgs& a, hipStream_t s);
 hipError_t launch_iov_emit(const IovArgs& a, hipStream_t s);
+// frame.hip
+hipError_t launch_frame_chunks(const FrameArgs& a, hipStream_t s);
+hipError_t launch_frame_write(const FrameArgs& a, hipStream_t s);
 // scan.hip
 hipError_t launch_scan_tiles(const uint64_t* in, uint64_t* out_excl, uint64_t count, uint64_t base,
                              uint64_t* total_out, hipStream_t s);

@@ -18,9 +18,10 @@ _LIB = None
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libonc_rpc_amd.so")
 
 K_NAMES = ["enc_len_kernel", "scan_tiles_kernel", "enc_emit_kernel", "decode_kernel",
-           "len_tiles_kernel", "len_apply_kernel", "enc_fixup_kernel", "iov_len_kernel", "iov_emit_kernel"]
+           "len_tiles_kernel", "len_apply_kernel", "enc_fixup_kernel", "iov_len_kernel", "iov_emit_kernel",
+           "frame_chunks_kernel", "frame_write_kernel"]
 (K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY, K_ENC_FIXUP, K_IOV_LEN,
- K_IOV_EMIT) = range(9)
+ K_IOV_EMIT, K_FRAME, K_FRAME_WRITE) = range(11)
 K_COUNT = len(K_NAMES)
 
 # every symbol include/onc_rpc.h declares
@@ -29,7 +30,7 @@ EXPORTED = [
     "onc_codec_sync", "onc_codec_reserve", "onc_codec_last_error", "onc_status_str",
     "onc_codec_enable_timing", "onc_codec_kernel_stats", "onc_codec_reset_stats",
     "onc_kernel_name", "onc_encode_lengths", "onc_encode", "onc_decode", "onc_scan_lengths",
-    "onc_expected_message_len", "onc_encode_iov",
+    "onc_expected_message_len", "onc_encode_iov", "onc_frame_stream",
 ]
 
 
@@ -75,6 +76,7 @@ def load_library(path=LIB_PATH):
     lib.onc_encode.argtypes = [vp, C.POINTER(OncBatch), vp, u64, vp, vp, vp]
     lib.onc_decode.argtypes = [vp, vp, vp, u64, i32, C.POINTER(OncDecoded)]
     lib.onc_scan_lengths.argtypes = [vp, vp, u64, u64, vp]
+    lib.onc_frame_stream.argtypes = [vp, vp, u64, vp, u64, vp]
     lib.onc_encode_iov.argtypes = [vp, C.POINTER(OncBatch), vp, u64, vp, vp, vp]
     lib.onc_expected_message_len.argtypes = [C.c_char_p, u64, C.POINTER(C.c_uint32)]
     lib.onc_expected_message_len.restype = C.c_int32
@@ -208,6 +210,11 @@ class Codec:
         self._check(self.lib.onc_encode_iov(self.h, C.byref(b), _ptr(hdr_out), cap, _ptr(iov), _ptr(status),
                                             _ptr(totals)), "onc_encode_iov")
 
+    def frame_stream(self, wire, length, rec_off, max_records, result):
+        """Frame a stream of back-to-back records (device buffers)."""
+        self._check(self.lib.onc_frame_stream(self.h, _ptr(wire), length, _ptr(rec_off), max_records,
+                                              _ptr(result)), "onc_frame_stream")
+
     # -- decode -----------------------------------------------------------
     def decode(self, wire, rec_off, n, mode, msgs, unix, status, aux0, aux1):
         d = OncDecoded(msgs.data_ptr(), unix.data_ptr(), status.data_ptr(), aux0.data_ptr(),
@@ -257,6 +264,21 @@ def encode_host_batch(codec: Codec, hb: L.HostBatch, device="cuda", out_cap=None
     codec.sync()
     return (out.cpu().numpy()[:min(total, cap)].tobytes(), rec_off.cpu().numpy().view(np.uint64).copy(),
             status.cpu().numpy()[:n].copy(), rec_len.cpu().numpy().view(np.uint32)[:n].copy())
+
+
+def frame_host_stream(codec: Codec, buf: bytes, max_records=None, device="cuda"):
+    """Convenience: host stream bytes -> GPU framing -> (rec_off[n+1], n, consumed, status, aux0, aux1)."""
+    torch = _torch()
+    w = to_device(np.frombuffer(bytes(buf) + b"\0" * 16, np.uint8), device)
+    m = len(buf) // 4 + 1 if max_records is None else max_records
+    off = torch.zeros(m + 1, dtype=torch.int64, device=device)
+    res = torch.zeros(5, dtype=torch.int64, device=device)
+    codec.frame_stream(w, len(buf), off, m, res)
+    codec.sync()
+    r = res.cpu().numpy()
+    n = int(r[0])
+    return (off.cpu().numpy().view(np.uint64)[:n + 1].copy(), n, int(r[1]), int(r[2]), int(np.uint32(r[3])),
+            int(np.uint32(r[4])))
 
 
 def codec_lengths(codec: Codec, db: DeviceBatch):

@@ -1001,6 +1001,45 @@ void oracle_decode_batch_mt(const uint8_t* wire, const uint64_t* rec_off, uint64
     for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
 }
 
+/* Framing of a byte stream of back-to-back records: the loop a caller of the
+ * reference runs over a socket buffer — expected_message_len
+ * (rpc_message.rs:343-367) on the remaining bytes, then a one-message slice
+ * of that length (the slice every TryFrom<&[u8]> requires,
+ * rpc_message.rs:238-242), until the buffer is used up or the next record
+ * is not complete. Writes up to max_records + 1 offsets; result =
+ * {n, consumed, status, aux0, aux1}: status ONC_OK when the buffer ends on a
+ * record boundary (or max_records were framed), else the expected_message_len
+ * error or IncompleteMessage{remaining bytes, wanted} for a record that runs
+ * past the end. */
+void oracle_frame_stream(const uint8_t* data, uint64_t len, uint64_t* rec_off, uint64_t max_records,
+                         uint64_t* result) {
+    uint64_t pos = 0, n = 0;
+    int32_t st = ONC_OK;
+    uint64_t aux0 = 0, aux1 = 0;
+    while (pos < len && n < max_records) {
+        uint32_t want = 0;
+        o_err e = expected_message_len(data + pos, len - pos, &want);
+        if (e.code != ONC_OK) {
+            st = e.code;
+            break;
+        }
+        if (len - pos < (uint64_t)want) {
+            st = ONC_ERR_INCOMPLETE_MESSAGE;
+            aux0 = len - pos;
+            aux1 = want;
+            break;
+        }
+        rec_off[n++] = pos;
+        pos += want;
+    }
+    rec_off[n] = pos;
+    result[0] = n;
+    result[1] = pos;
+    result[2] = (uint64_t)(int64_t)st;
+    result[3] = aux0;
+    result[4] = aux1;
+}
+
 /* Multi-threaded batch encode (CPU-baseline leg only): what a multi-core
  * caller of the reference does — serialised_len() per record
  * (src/rpc_message.rs:201-204) on every thread, an exclusive scan of the

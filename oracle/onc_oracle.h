@@ -67,6 +67,10 @@ void oracle_encode_batch_mt(uint64_t n, const onc_msg* msgs, const onc_unix_para
                             const uint8_t* auth_arena, const uint8_t* payload_arena, uint8_t* out,
                             uint64_t* rec_off, int32_t* status, uint32_t* rec_len, int threads);
 
+/* The caller's expected_message_len loop over a stream buffer (framing). */
+void oracle_frame_stream(const uint8_t* data, uint64_t len, uint64_t* rec_off, uint64_t max_records,
+                         uint64_t* result);
+
 /* Component-level entry points used by the golden-vector tests. */
 /* expected_message_len — src/rpc_message.rs:343-367 */
 int32_t oracle_expected_message_len(const uint8_t* data, uint64_t len, uint32_t* out);

@@ -34,6 +34,8 @@ def load():
     lib.oracle_decode_batch_mt.restype = None
     lib.oracle_encode_batch_mt.argtypes = [u64, vp, vp, vp, vp, vp, vp, vp, vp, i32]
     lib.oracle_encode_batch_mt.restype = None
+    lib.oracle_frame_stream.argtypes = [vp, u64, vp, u64, vp]
+    lib.oracle_frame_stream.restype = None
     lib.oracle_expected_message_len.argtypes = [vp, u64, vp]
     lib.oracle_expected_message_len.restype = C.c_int32
     lib.oracle_auth_decode.argtypes = [vp, u64, i32, vp, vp, vp]
@@ -122,6 +124,18 @@ def decode_batch(wire, rec_off, mode, threads=1):
         lib.oracle_decode_batch(_p(wire), _p(rec_off), n, mode, _p(msgs), _p(unix), _p(status),
                                 _p(aux0), _p(aux1))
     return msgs[:n], unix[:2 * n], status[:n], aux0[:n], aux1[:n]
+
+
+def frame_stream(buf, max_records=None):
+    """Caller's expected_message_len loop -> (rec_off u64[n+1], n, consumed, status, aux0, aux1)."""
+    lib = load()
+    a = np.frombuffer(bytes(buf) + b"\0" * 8, np.uint8).copy()
+    n_max = len(buf) // 4 + 1 if max_records is None else max_records
+    off = np.zeros(n_max + 1, np.uint64)
+    res = np.zeros(5, np.uint64)
+    lib.oracle_frame_stream(_p(a), len(buf), _p(off), n_max, _p(res))
+    n = int(res[0])
+    return off[:n + 1], n, int(res[1]), int(np.int64(res[2])), int(res[3]), int(res[4])
 
 
 def decode_message(buf: bytes, mode):

@@ -442,3 +442,55 @@ def test_parse_serialise_fuzz_invariant(codec, R, oracle):
     assert (hs == 0).all()
     for j, i in enumerate(ok):
         assert L.describe(hm[j], hu, w2) == L.describe(gm[i], gu, cw), int(i)
+
+
+# ---------------------------------------------------------------------------
+# Stream framing vs the caller's expected_message_len loop
+def _frame_both(R, codec, oracle, buf, max_records=None):
+    g = R.frame_host_stream(codec, buf, max_records)
+    o = oracle.frame_stream(buf, max_records)
+    assert g[1:] == o[1:], (g[1:], o[1:])
+    assert np.array_equal(g[0], o[0])
+    return o
+
+
+def test_frame_stream_valid_streams(codec, R, oracle):
+    for hb in (S.call_none(5000, 256), S.mixed(3000, seed=3, pmin=0, pmax=5000, exotic=0.2),
+               L.build_batch(S.random_messages(3000, seed=8, max_payload=300))):
+        wire = oracle.encode_batch(hb)[0]
+        o = _frame_both(R, codec, oracle, wire)
+        assert o[1] == int((oracle.encode_batch(hb)[2] == 0).sum()) and o[3] == 0
+        # every cut inside the stream: incomplete tails
+        for cut in (len(wire) - 1, len(wire) - 3, len(wire) // 2, 5, 2, 0):
+            _frame_both(R, codec, oracle, wire[:cut])
+        for m in (1, 7, hb.n // 2, hb.n - 1, hb.n, hb.n + 5):
+            _frame_both(R, codec, oracle, wire, max_records=m)
+
+
+def test_frame_stream_adversarial(codec, R, oracle):
+    rng = np.random.default_rng(4)
+    # payloads that are themselves RPC streams (nested records fool the guess)
+    inner = oracle.encode_batch(S.mixed(400, seed=9, pmin=0, pmax=900))[0]
+    msgs = []
+    for i in range(600):
+        k = int(rng.integers(0, len(inner) - 2000))
+        msgs.append({"xid": i, "type": "call", "program": 1, "program_version": 1, "procedure": 1,
+                     "cred": {"kind": "none", "data": None}, "verf": {"kind": "none", "data": None},
+                     "payload": inner[k:k + int(rng.integers(0, 2000))].hex()})
+    wire = oracle.encode_batch(L.build_batch(msgs))[0]
+    _frame_both(R, codec, oracle, wire)
+    # tiny and empty-body records (4..20 bytes), huge records spanning chunks
+    parts = []
+    for i in range(3000):
+        kind = int(rng.integers(0, 3))
+        body = rng.bytes(int(rng.integers(0, 17)) if kind < 2 else int(rng.integers(3000, 9000)))
+        parts.append(((len(body)) | 0x80000000).to_bytes(4, "big") + body)
+    stream = b"".join(parts)
+    _frame_both(R, codec, oracle, stream)
+    # a fragmented header, and random garbage after a valid prefix
+    bad = bytearray(stream)
+    j = len(b"".join(parts[:1500]))
+    bad[j] &= 0x7F
+    _frame_both(R, codec, oracle, bytes(bad))
+    _frame_both(R, codec, oracle, stream[:j] + rng.bytes(50000))
+    _frame_both(R, codec, oracle, rng.bytes(100000))
