@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--workload", choices=["c1", "c2", "c3"], default="c1")
     ap.add_argument("--records", type=int, default=None, help="records per GPU")
     ap.add_argument("--mode", choices=["slice", "bytes"], default="slice")
+    ap.add_argument("--frame", action="store_true",
+                    help="c2: frame the raw stream on the device (onc_frame_stream) instead of scanning rec_len")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pcie-reps", type=int, default=3)
@@ -184,7 +186,8 @@ def main():
         desc = "configs[1]: Call(prog 100003, vers 4, proc 1, AuthNone(None) x2) + 256 B payload, encode -> decode"
     elif wl == "c2":
         hb = S.mixed(n, seed=2 + rank)
-        desc = "configs[2]: mixed Call/Reply (payloads 64..4096 B), rec_len scan + decode"
+        desc = ("configs[2]: mixed Call/Reply (payloads 64..4096 B), " +
+                ("device stream framing" if args.frame else "rec_len scan") + " + decode")
     else:
         hb = S.call_unix16(n, 1024, seed=3 + rank)
         desc = "configs[3]: Call(AuthUnix 16 gids) + AuthNone + 1 KiB payload, encode -> decode"
@@ -210,8 +213,13 @@ def main():
         torch.cuda.synchronize()
         dec_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
 
+        frame_res = torch.zeros(5, dtype=torch.int64, device=dev)
+
         def step():
-            codec.scan_lengths(rec_len, n, 0, dec_off)
+            if args.frame:
+                codec.frame_stream(out, total_bytes, dec_off, n, frame_res)
+            else:
+                codec.scan_lengths(rec_len, n, 0, dec_off)
             codec.decode(out, dec_off, n, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1)
     else:
         def step():
@@ -347,6 +355,10 @@ def main():
         "len_tiles_kernel": 4 * n,
         "len_apply_kernel": 12 * n,
         "enc_fixup_kernel": 0,                   # deferred tiles only
+        "iov_len_kernel": 0,
+        "iov_emit_kernel": 0,
+        "frame_chunks_kernel": 0,
+        "frame_write_kernel": 8 * n,
     }
     kern = {}
     for name, (tot_ms, cnt) in breakdown.items():

@@ -527,8 +527,20 @@ public:
     std::vector<Decoded> try_from(Codec& codec, const uint8_t* wire, size_t wire_len,
                                   const std::vector<uint32_t>& rec_len, DecodeMode mode = DecodeMode::Slice);
 
+    // A socket read buffer of back-to-back records: frame it on the device
+    // (the caller's expected_message_len loop, rpc_message.rs:343-367), then
+    // decode every complete record. `consumed` receives the bytes used;
+    // `stop` why framing stopped before the end (nullopt when the buffer
+    // ended on a record boundary): an incomplete trailing record means
+    // "read more", as with the reference.
+    std::vector<Decoded> try_from_stream(Codec& codec, const uint8_t* wire, size_t wire_len,
+                                         DecodeMode mode = DecodeMode::Slice, size_t* consumed = nullptr,
+                                         std::optional<Error>* stop = nullptr);
+
 private:
-    detail::DevBuf d_wire_, d_len_, d_off_, d_msgs_, d_unix_, d_status_, d_aux0_, d_aux1_;
+    std::vector<Decoded> decode_device(Codec& codec, const uint8_t* wire, const uint8_t* dw, size_t n,
+                                       const uint64_t* doff, DecodeMode mode);
+    detail::DevBuf d_wire_, d_len_, d_off_, d_msgs_, d_unix_, d_status_, d_aux0_, d_aux1_, d_res_;
 };
 
 // expected_message_len (rpc_message.rs:343-367); throws Error.
@@ -732,18 +744,11 @@ inline RpcMessage message_view(const onc_msg& d, const onc_unix_params* unix, co
 
 }  // namespace detail
 
-inline std::vector<Decoded> BatchDecoder::try_from(Codec& codec, const uint8_t* wire, size_t wire_len,
-                                                   const std::vector<uint32_t>& rec_len, DecodeMode mode) {
+inline std::vector<Decoded> BatchDecoder::decode_device(Codec& codec, const uint8_t* wire, const uint8_t* dw,
+                                                        size_t n, const uint64_t* doff, DecodeMode mode) {
     using detail::hip_check;
-    const size_t n = rec_len.size();
     std::vector<Decoded> res(n);
     if (!n) return res;
-    uint8_t* dw = static_cast<uint8_t*>(d_wire_.ensure(wire_len + 16));
-    if (wire_len) hip_check(hipMemcpy(dw, wire, wire_len, hipMemcpyHostToDevice), "H2D");
-    uint32_t* dl = static_cast<uint32_t*>(d_len_.ensure(n * 4));
-    hip_check(hipMemcpy(dl, rec_len.data(), n * 4, hipMemcpyHostToDevice), "H2D");
-    uint64_t* doff = static_cast<uint64_t*>(d_off_.ensure((n + 1) * 8));
-    codec.check(onc_scan_lengths(codec.get(), dl, n, 0, doff), "onc_scan_lengths");
     onc_decoded out{};
     out.msgs = static_cast<onc_msg*>(d_msgs_.ensure(n * sizeof(onc_msg)));
     out.unix_params = static_cast<onc_unix_params*>(d_unix_.ensure(2 * n * sizeof(onc_unix_params)));
@@ -768,6 +773,41 @@ inline std::vector<Decoded> BatchDecoder::try_from(Codec& codec, const uint8_t* 
         if (st[i] == ONC_OK) res[i].message = detail::message_view(msgs[i], unix.data(), wire);
     }
     return res;
+}
+
+inline std::vector<Decoded> BatchDecoder::try_from(Codec& codec, const uint8_t* wire, size_t wire_len,
+                                                   const std::vector<uint32_t>& rec_len, DecodeMode mode) {
+    using detail::hip_check;
+    const size_t n = rec_len.size();
+    if (!n) return {};
+    uint8_t* dw = static_cast<uint8_t*>(d_wire_.ensure(wire_len + 16));
+    if (wire_len) hip_check(hipMemcpy(dw, wire, wire_len, hipMemcpyHostToDevice), "H2D");
+    uint32_t* dl = static_cast<uint32_t*>(d_len_.ensure(n * 4));
+    hip_check(hipMemcpy(dl, rec_len.data(), n * 4, hipMemcpyHostToDevice), "H2D");
+    uint64_t* doff = static_cast<uint64_t*>(d_off_.ensure((n + 1) * 8));
+    codec.check(onc_scan_lengths(codec.get(), dl, n, 0, doff), "onc_scan_lengths");
+    return decode_device(codec, wire, dw, n, doff, mode);
+}
+
+inline std::vector<Decoded> BatchDecoder::try_from_stream(Codec& codec, const uint8_t* wire, size_t wire_len,
+                                                          DecodeMode mode, size_t* consumed,
+                                                          std::optional<Error>* stop) {
+    using detail::hip_check;
+    uint8_t* dw = static_cast<uint8_t*>(d_wire_.ensure(wire_len + 16));
+    if (wire_len) hip_check(hipMemcpy(dw, wire, wire_len, hipMemcpyHostToDevice), "H2D");
+    const size_t max_records = wire_len / 4 + 1;   // every record is at least 4 bytes
+    uint64_t* doff = static_cast<uint64_t*>(d_off_.ensure((max_records + 1) * 8));
+    uint64_t* dres = static_cast<uint64_t*>(d_res_.ensure(5 * 8));
+    codec.check(onc_frame_stream(codec.get(), dw, wire_len, doff, max_records, dres), "onc_frame_stream");
+    codec.sync();
+    uint64_t r[5];
+    hip_check(hipMemcpy(r, dres, sizeof(r), hipMemcpyDeviceToHost), "D2H");
+    if (consumed) *consumed = size_t(r[1]);
+    if (stop) {
+        if (int32_t(r[2]) == ONC_OK) *stop = std::nullopt;
+        else *stop = Error(int32_t(r[2]), uint32_t(r[3]), uint32_t(r[4]));
+    }
+    return decode_device(codec, wire, dw, size_t(r[0]), doff, mode);
 }
 
 // ----------------------------------------------------------------------------

@@ -7,3 +7,4 @@ for wl in c1 c2 c3; do
   rc=$?; echo "bench $wl rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
+timeout -k 10 400 python bench.py --workload c2 --frame ${BENCH_ARGS:-} > gpurun_out/bench_c2f.log 2>&1; rc=$?; echo "bench c2f rc=$rc"; [ $rc -eq 0 ] || exit $rc

@@ -304,6 +304,33 @@ static void test_batch_round_trip(Codec& c) {
     }
 }
 
+// The caller's loop over a socket buffer (expected_message_len + one-message
+// slices), done on the device: BatchDecoder::try_from_stream.
+static void test_stream_framing(Codec& c) {
+    const std::vector<uint8_t> a = fixture("call_auth_unix_16gids_288B");
+    const std::vector<uint8_t> b = fixture("reply_accepted_success_76B");
+    std::vector<uint8_t> stream;
+    for (int i = 0; i < 500; ++i) {
+        const std::vector<uint8_t>& r = (i % 3) ? a : b;
+        stream.insert(stream.end(), r.begin(), r.end());
+    }
+    BatchDecoder dec;
+    size_t consumed = 0;
+    std::optional<Error> stop;
+    std::vector<Decoded> out = dec.try_from_stream(c, stream.data(), stream.size(), DecodeMode::Slice, &consumed, &stop);
+    CHECK(out.size() == 500 && consumed == stream.size() && !stop.has_value());
+    for (int i = 0; i < 500; ++i) {
+        CHECK(out[i].ok());
+        CHECK(out[i].message->xid() == ((i % 3) ? 643743997u : 643743997u));
+        CHECK((out[i].message->call_body() != nullptr) == bool(i % 3));
+    }
+    // a partial trailing record: "read more" (IncompleteMessage), 499 framed
+    out = dec.try_from_stream(c, stream.data(), stream.size() - 10, DecodeMode::Bytes, &consumed, &stop);
+    CHECK(out.size() == 499 && consumed == stream.size() - a.size());
+    CHECK(stop.has_value() && stop->code() == ONC_ERR_INCOMPLETE_MESSAGE);
+    CHECK(stop->buffer_len() == a.size() - 10 && stop->expected() == a.size());
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s vectors.json\n", argv[0]);
@@ -328,6 +355,7 @@ int main(int argc, char** argv) {
         {"test_panics", test_panics},
         {"test_expected_message_len", test_expected_message_len},
         {"test_batch_round_trip", test_batch_round_trip},
+        {"test_stream_framing", test_stream_framing},
     };
     for (const auto& t : tests) {
         try {
