@@ -361,8 +361,9 @@ int onc_encode_iov(onc_codec* c, const onc_batch* batch, uint8_t* hdr_out, uint6
     return run(c, ONC_K_IOV_EMIT, "iov_emit", [&] { return onc::launch_iov_emit(a, c->stream); });
 }
 
-// Per-chunk framing state: 56 bytes per chunk + the count scan's tile sums.
-static size_t frame_bytes(uint64_t P) { return P * 56 + (onc::num_tiles(P) + 1) * 16 + 64; }
+// Per-chunk framing state: 56 bytes per chunk + summary flags + the count
+// scan's tile sums.
+static size_t frame_bytes(uint64_t P) { return P * 56 + 2 * (P / 256 + 2) + 2 * (P / 65536 + 2) + (onc::num_tiles(P) + 1) * 16 + 128; }
 
 int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* rec_off, uint64_t max_records,
                      uint64_t* result) {
@@ -403,6 +404,12 @@ int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* 
     a.st = reinterpret_cast<int32_t*>(f + 36 * Q);
     a.cnt_eff = reinterpret_cast<uint32_t*>(f + 40 * Q);
     a.fail = f + 44 * Q;
+    a.stop = f + 45 * Q;
+    uint8_t* flags = f + 46 * Q;   // 10 bytes per chunk remain in the 56-byte budget
+    a.fail2 = flags;
+    a.stop2 = flags + (Q / 256 + 2);
+    a.fail3 = flags + 2 * (Q / 256 + 2);
+    a.stop3 = a.fail3 + (Q / 65536 + 2);
     uint64_t* tail = reinterpret_cast<uint64_t*>(f + 56 * Q);
     const uint64_t nt = onc::num_tiles(P);
     uint64_t* tile_sum = tail;

@@ -85,10 +85,11 @@ __device__ __forceinline__ uint64_t tile_start(const EncArgs& a, uint64_t tile) 
 // ---------------------------------------------------------------------------
 // enc_emit: the hot kernel (word-aligned tiles).
 // ---------------------------------------------------------------------------
-constexpr int kFastHdrCap = 2048;             // header words per wave tile (8 KiB of LDS)
+constexpr int kFastHdrCap = 1024;             // header words per span (4 KiB of LDS)
+static_assert(8 * (7 + 2 * 52) <= kFastHdrCap, "a span of 8 maximal headers must fit LDS");
 constexpr int kFastMapCap = 1024;             // output granules per wave tile
 constexpr int kFastWaves = 4;                 // wave tiles per workgroup
-constexpr int kEmitUnroll = 2;                // output chunks per lane per step
+constexpr int kEmitUnroll = 1;                // output chunks per lane per step
 
 // Per-record LDS entry of enc_emit (two ds_read_b128).
 struct FastEnt {
@@ -100,9 +101,9 @@ struct FastEnt {
 };
 
 struct FastTile {
-    FastEnt ent[kEmitRecs + 1];      // [nrec] = sentinel {T1, T1, 0, 0, 0}
-    uint32_t hdr[kFastHdrCap];       // header words of the tile's records (stream order)
-    uint8_t map[kFastMapCap];        // granule -> record holding its first in-tile byte
+    FastEnt ent[kEmitRecs + 1];      // [span records] = sentinel {S1, S1, 0, 0, 0}
+    uint32_t hdr[kFastHdrCap];       // header words of the span's records (stream order)
+    uint8_t map[kFastMapCap];        // granule -> span record holding its first byte
 };
 
 // enc_emit: every wavefront owns one tile of kEmitRecs = 64 records and
@@ -139,15 +140,15 @@ __global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) 
     const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
     const uintptr_t payload = reinterpret_cast<uintptr_t>(a.payload_arena);
 
-    onc_msg d;
-    uint64_t len = 0;
+    uint64_t len = 0, poff = 0;
     uint32_t hw = 0;
     bool word_aligned = true;
     if (lane < nrec) {
-        d = a.msgs[r0 + lane];
+        const onc_msg d = a.msgs[r0 + lane];
         const RecPlan p = plan_record(d, a.unix);
         len = p.len;
         hw = len ? meta_hw(p.meta) : 0;
+        poff = d.payload_off;
         word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((payload + d.payload_off) & 3) == 0);
     }
     // One wave scan places output bytes and LDS header words: (len << 16 | hw).
@@ -158,77 +159,98 @@ __global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) 
     const uint64_t en = start + len;
     const uint64_t pst = start + 4ull * hw;
     const uint32_t hoff = uint32_t(excl & 0xFFFFu);
-    const uint64_t last = __shfl(incl, nrec - 1, 64);
-    const uint64_t T1 = T0 + (last >> 16);
+    const uint32_t hincl = uint32_t(incl & 0xFFFFu);
     if (lane < nrec) {
         a.rec_off[r0 + lane] = start;
         if (len != 0 && en > a.out_cap) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
     }
-    const bool fast = __all(word_aligned) && (T0 & 3) == 0 && (last & 0xFFFFu) <= uint64_t(kFastHdrCap);
+    const bool fast = __all(word_aligned) && (T0 & 3) == 0;
     if (lane == 0) a.tile_base[tile] = T0 | (fast ? 0 : kDeferBit);
     if (!fast) return;
-    const int32_t dw = int32_t(hoff) - int32_t((start - T0) >> 2);
-    const int32_t dwn_raw = __shfl_down(dw, 1, 64);
-    if (lane < nrec) {
-        const uint64_t srcbase = payload + d.payload_off - pst;
-        T.ent[lane] = FastEnt{pst, en, srcbase, dw, lane + 1 < nrec ? dwn_raw : dw};
-        if (len != 0) {
-            const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
-            put_header_words(d, uint32_t(len), src, &T.hdr[hoff]);
-        }
-    }
-    // granule size: 64 B, doubled until the tile's bytes fit the map
-    uint32_t gs = 6;
-    while (((T1 - T0) >> gs) >= uint64_t(kFastMapCap)) ++gs;
-    const uint64_t G0 = T0 >> gs;
-    if (lane < nrec && len != 0) {
-        // claim the granules whose first byte lies in this record
-        const uint64_t gsz = 1ull << gs;
-        for (uint64_t g = (start + gsz - 1) >> gs; g <= (en - 1) >> gs; ++g) T.map[g - G0] = uint8_t(lane);
-    }
-    if (lane == 0) {
-        T.ent[nrec] = FastEnt{T1, T1, 0, 0, 0};
-        if (T0 & ((1ull << gs) - 1)) T.map[0] = 0;   // granule 0 starts before the tile
-    }
-    wave_lds_sync();
 
-    const uint64_t E = min(T1, a.out_cap);
-    if (E <= T0) return;                              // no bytes (all records failed, or beyond out_cap)
+    // Spans: the tile's records in groups of S (64, 32, 16 or 8) whose header
+    // words fit kFastHdrCap (8 records always fit: <= 111 words each).
+    int S = kEmitRecs;
+    for (; S > 8; S >>= 1) {
+        const int g0 = lane & ~(S - 1);
+        const int g1 = min(lane | (S - 1), nrec - 1);
+        const uint32_t top = __shfl(hincl, g1, 64);
+        const uint32_t bot = __shfl(hoff, g0, 64);
+        if (!__any(g0 < nrec && top - bot > uint32_t(kFastHdrCap))) break;
+    }
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.msgs);   // >= 64 valid bytes
-    // kU chunks per lane per step: their loads are all in flight before the
-    // first store (more bytes in flight per wave).
-    const uint64_t cend = (E + 15) >> 4;
-    for (uint64_t c = (T0 >> 4) + lane; c < cend; c += 64 * kU) {
-        uint32_t v[kU][4];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const uint64_t o = (c + 64 * u) << 4;
-            const uint64_t lo = max(o, T0);
-            if (c + 64 * u >= cend) break;
-            int r = T.map[(lo >> gs) - G0];
-            FastEnt e = T.ent[r];
-            while (lo >= e.en) e = T.ent[++r];            // sentinel en = T1 > lo
-            if (o >= e.pst && o + 16 <= e.en) {
-                load16_unaligned(e.srcbase + o, v[u]);
-            } else {
-                const int64_t q = (int64_t(o) - int64_t(T0)) >> 2;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint64_t p = o + 4 * i;
-                    const bool in_pay = p >= e.pst && p < e.en;
-                    const int64_t hidx = q + i + (p >= e.en ? e.dwn : e.dw);
-                    const int64_t hcl = hidx < 0 ? 0 : (hidx >= kFastHdrCap ? kFastHdrCap - 1 : hidx);
-                    const uint32_t h = T.hdr[hcl];
-                    const uint32_t w = gload<uint32_t>(in_pay ? e.srcbase + p : dummy);
-                    v[u][i] = in_pay ? w : h;
-                }
+    for (int lo_rec = 0; lo_rec < nrec; lo_rec += S) {
+        const int hi_rec = min(nrec, lo_rec + S);
+        const int ns = hi_rec - lo_rec;
+        const uint64_t S0 = __shfl(start, lo_rec, 64);
+        const uint64_t S1 = __shfl(en, hi_rec - 1, 64);
+        const uint32_t hb = __shfl(hoff, lo_rec, 64);
+        if (lo_rec) wave_lds_sync();                   // the previous span's readers are done
+        const bool active = lane >= lo_rec && lane < hi_rec;
+        const int j = lane - lo_rec;
+        const int32_t dw = int32_t(hoff - hb) - int32_t((start - S0) >> 2);
+        const int32_t dwn_raw = __shfl_down(dw, 1, 64);
+        if (active) {
+            T.ent[j] = FastEnt{pst, en, payload + poff - pst, dw, lane + 1 < hi_rec ? dwn_raw : dw};
+            if (len != 0) {
+                // descriptor re-read (L2) rather than kept live across the spans
+                const onc_msg d = a.msgs[r0 + lane];
+                const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
+                put_header_words(d, uint32_t(len), src, &T.hdr[hoff - hb]);
             }
         }
+        // granule size: 64 B, doubled until the span's bytes fit the map
+        uint32_t gs = 6;
+        while (((S1 - S0) >> gs) >= uint64_t(kFastMapCap)) ++gs;
+        const uint64_t G0 = S0 >> gs;
+        if (active && len != 0) {
+            // claim the granules whose first byte lies in this record
+            const uint64_t gsz = 1ull << gs;
+            for (uint64_t g = (start + gsz - 1) >> gs; g <= (en - 1) >> gs; ++g) T.map[g - G0] = uint8_t(j);
+        }
+        if (lane == 0) {
+            T.ent[ns] = FastEnt{S1, S1, 0, 0, 0};
+            if (S0 & ((1ull << gs) - 1)) T.map[0] = 0;   // granule 0 starts before the span
+        }
+        wave_lds_sync();
+
+        const uint64_t E = min(S1, a.out_cap);
+        if (E <= S0) continue;                        // no bytes (all records failed, or beyond out_cap)
+        // kU chunks per lane per step: their loads are all in flight before
+        // the first store.
+        const uint64_t cend = (E + 15) >> 4;
+        for (uint64_t c = (S0 >> 4) + lane; c < cend; c += 64 * kU) {
+            uint32_t v[kU][4];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const uint64_t o = (c + 64 * u) << 4;
-            if (c + 64 * u >= cend) break;
-            store_chunk(a.out, o, max(o, T0), min(o + 16, E), v[u]);
+            for (int u = 0; u < kU; ++u) {
+                const uint64_t o = (c + 64 * u) << 4;
+                const uint64_t lo = max(o, S0);
+                if (c + 64 * u >= cend) break;
+                int r = T.map[(lo >> gs) - G0];
+                FastEnt e = T.ent[r];
+                while (lo >= e.en) e = T.ent[++r];        // sentinel en = S1 > lo
+                if (o >= e.pst && o + 16 <= e.en) {
+                    load16_unaligned(e.srcbase + o, v[u]);
+                } else {
+                    const int64_t q = (int64_t(o) - int64_t(S0)) >> 2;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint64_t p = o + 4 * i;
+                        const bool in_pay = p >= e.pst && p < e.en;
+                        const int64_t hidx = q + i + (p >= e.en ? e.dwn : e.dw);
+                        const int64_t hcl = hidx < 0 ? 0 : (hidx >= kFastHdrCap ? kFastHdrCap - 1 : hidx);
+                        const uint32_t h = T.hdr[hcl];
+                        const uint32_t w = gload<uint32_t>(in_pay ? e.srcbase + p : dummy);
+                        v[u][i] = in_pay ? w : h;
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint64_t o = (c + 64 * u) << 4;
+                if (c + 64 * u >= cend) break;
+                store_chunk(a.out, o, max(o, S0), min(o + 16, E), v[u]);
+            }
         }
     }
 }

@@ -7,7 +7,7 @@
 // record k's header: a serial chain. Here it is framed in parallel by
 // speculation + verification, with the same result as the serial loop:
 //
-//   frame_chunks  lane per 1 KiB chunk: guess the first record start in the
+//   frame_chunks  lane per 4 KiB chunk: guess the first record start in the
 //                 chunk (the first position that looks like an ONC-RPC
 //                 header: last-fragment bit, length within the buffer,
 //                 message type 0 with rpcvers 2 or 1 with reply_stat 0/1),
@@ -75,38 +75,85 @@ __device__ __forceinline__ Chase chase(const FrameArgs& a, uint64_t p, uint64_t 
     return c;
 }
 
+// Full plausibility test of a record start at p (p + 16 <= len).
+// Beyond the record mark and message type: a call has rpcvers 2 and a
+// credential length <= 200 (flavor.rs:83); a reply has reply_stat 0 with a
+// verifier length <= 200, or reply_stat 1 with a rejection kind 0/1. Every
+// record the reference's decoder accepts passes; the test only steers the
+// guess (a record that fails it is still framed, via the walk).
+__device__ __forceinline__ bool plausible_at(const FrameArgs& a, uint64_t p) {
+    const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
+    const uint32_t h = be_at(base, p);
+    const uint32_t mt = be_at(base, p + 8);
+    const uint32_t rv = be_at(base, p + 12);
+    const uint64_t want = uint64_t(h & 0x7FFFFFFFu) + 4;
+    if (!(h & 0x80000000u) || want < 24 || want > a.len - p) return false;
+    if (mt == 0) return rv == 2u && want >= 44 && be_at(base, p + 32) <= ONC_MAX_AUTH_LEN;
+    if (mt != 1 || rv > 1u) return false;
+    const uint32_t w4 = be_at(base, p + 16), w5 = be_at(base, p + 20);
+    return rv == 0 ? (want >= 28 && w5 <= ONC_MAX_AUTH_LEN) : w4 <= 1u;
+}
+
+// 4-bit mask of the zero bytes / high-bit bytes of a dword.
+__device__ __forceinline__ uint32_t zero_nibble(uint32_t w) {
+    const uint32_t z = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);   // 0x80 in each zero byte
+    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+__device__ __forceinline__ uint32_t high_nibble(uint32_t w) {
+    const uint32_t z = w & 0x80808080u;
+    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+
 // First position in [c0, c1) whose bytes look like a record start (a guess:
 // correctness never depends on it). 64 positions per step from an 80-byte
-// register window of five aligned 16-byte loads.
+// register window (five aligned 16-byte loads): a record start has its
+// last-fragment bit set and a message type word of 0 or 1, i.e. three zero
+// bytes at +8..+10; byte masks of the window select the candidates, and only
+// those get the full test.
 __device__ __forceinline__ uint64_t guess_start(const FrameArgs& a, uint64_t c0, uint64_t c1) {
     const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
     const uint64_t lastblk = (a.len - 1) & ~uint64_t(15);   // last 16-byte block holding a buffer byte
     for (uint64_t blk = c0 & ~uint64_t(15); blk < c1; blk += 64) {
-        uint32_t w[20];
+        uint64_t Z0 = 0, H0 = 0;
+        uint32_t Z1 = 0;
 #pragma unroll
         for (int b = 0; b < 5; ++b) {
             const uint64_t o = blk + 16 * b;
             const u32x4 v = gload<u32x4>(base + (o <= lastblk ? o : lastblk));
-            w[4 * b] = v.x;
-            w[4 * b + 1] = v.y;
-            w[4 * b + 2] = v.z;
-            w[4 * b + 3] = v.w;
-        }
-        uint64_t hit = 0;
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int k = 0; k < 64; ++k) {
-            const uint64_t p = blk + k;
-            const uint32_t sh = k & 3;
-            const int wi = k >> 2;
-            const uint32_t h = bswap(funnel(w[wi], w[wi + 1], sh));
-            const uint32_t mt = bswap(funnel(w[wi + 2], w[wi + 3], sh));
-            const uint32_t rv = bswap(funnel(w[wi + 3], w[wi + 4], sh));
-            const uint64_t want = uint64_t(h & 0x7FFFFFFFu) + 4;
-            const bool plausible = (h & 0x80000000u) && want >= 24 && p + 16 <= a.len && want <= a.len - p &&
-                                   (mt == 0 ? rv == 2u : (mt == 1 && rv <= 1u)) && p >= c0 && p < c1;
-            hit |= uint64_t(plausible) << k;
+            for (int i = 0; i < 4; ++i) {
+                const int d = 4 * b + i;
+                if (d < 16) {
+                    Z0 |= uint64_t(zero_nibble(w[i])) << (4 * d);
+                    H0 |= uint64_t(high_nibble(w[i])) << (4 * d);
+                } else {
+                    Z1 |= zero_nibble(w[i]) << (4 * (d - 16));
+                }
+            }
         }
-        if (hit) return blk + __ffsll(static_cast<unsigned long long>(hit)) - 1;
+        // bit k: bytes k+8, k+9, k+10 are zero (80-bit Z = Z1:Z0)
+        const uint64_t z8 = (Z0 >> 8) | (uint64_t(Z1) << 56);
+        const uint64_t z9 = (Z0 >> 9) | (uint64_t(Z1) << 55);
+        const uint64_t z10 = (Z0 >> 10) | (uint64_t(Z1) << 54);
+        uint64_t cand = H0 & z8 & z9 & z10;
+        // positions inside [c0, c1) with 16 bytes of buffer
+        const uint64_t lo = c0 > blk ? c0 - blk : 0;
+        const uint64_t hi_pos = min(c1, a.len >= 16 ? a.len - 15 : 0);   // p < hi_pos
+        const uint64_t hi = hi_pos > blk ? min(uint64_t(64), hi_pos - blk) : 0;
+        cand &= (hi >= 64 ? ~0ull : ((1ull << hi) - 1)) & ~((1ull << lo) - 1);
+        while (cand) {
+            const uint64_t p = blk + __ffsll(static_cast<unsigned long long>(cand)) - 1;
+            if (plausible_at(a, p)) {
+                // and the record it claims is followed by another plausible
+                // start (or the buffer's end): rejects words inside a record
+                // that happen to look like a header (e.g. the xid of a
+                // denied reply, whose next words are 1, 1, 1).
+                const uint64_t q = p + uint64_t(be_at(base, p) & 0x7FFFFFFFu) + 4;
+                if (q + 16 > a.len || plausible_at(a, q)) return p;
+            }
+            cand &= cand - 1;
+        }
     }
     return kNone;
 }
@@ -125,6 +172,8 @@ __global__ __launch_bounds__(256) void frame_chunks_kernel(FrameArgs a) {
         *a.first_fail = kNone;
         *a.first_stop = kNone;
     }
+    if (t < ((a.nchunks + 255) >> 8)) a.fail2[t] = a.stop2[t] = 0;
+    if (t < ((a.nchunks + 65535) >> 16)) a.fail3[t] = a.stop3[t] = 0;
     if (t >= a.nchunks) return;
     const uint64_t c0 = t * kFrameChunk;
     const uint64_t c1 = min(c0 + kFrameChunk, a.len);
@@ -138,11 +187,14 @@ __global__ __launch_bounds__(256) void frame_chunks_kernel(FrameArgs a) {
 }
 
 // fail[t] = 1 when guessed chunk t's chain does not land on a guess, or jumps
-// over a guessed chunk; first_stop = first guessed chunk whose chain ends.
+// over a guessed chunk; stop[t] = 1 when guessed chunk t's chain ends there.
+// Both also set their per-256-chunk and per-65536-chunk summary flags (zeroed
+// by frame_chunks) so that the walk finds the next set flag in three short
+// ballot scans; first_fail / first_stop = the minimum flagged chunk.
 __global__ __launch_bounds__(256) void frame_verify_kernel(FrameArgs a) {
     const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (t >= a.nchunks) return;
-    uint8_t bad = 0;
+    uint8_t bad = 0, stop = 0;
     const uint64_t g = a.g[t];
     if (g != kNone) {
         if (a.st[t] == kExit) {
@@ -152,24 +204,55 @@ __global__ __launch_bounds__(256) void frame_verify_kernel(FrameArgs a) {
             for (uint64_t k = t + 1; k < j && !bad; ++k)
                 if (a.g[k] != kNone) bad = 1;
         } else {
-            atomicMin(reinterpret_cast<unsigned long long*>(a.first_stop), static_cast<unsigned long long>(t));
+            stop = 1;
         }
     }
     a.fail[t] = bad;
-    if (bad) atomicMin(reinterpret_cast<unsigned long long*>(a.first_fail), static_cast<unsigned long long>(t));
+    a.stop[t] = stop;
+    if (bad) {
+        a.fail2[t >> 8] = 1;
+        a.fail3[t >> 16] = 1;
+        atomicMin(reinterpret_cast<unsigned long long*>(a.first_fail), static_cast<unsigned long long>(t));
+    }
+    if (stop) {
+        a.stop2[t >> 8] = 1;
+        a.stop3[t >> 16] = 1;
+        atomicMin(reinterpret_cast<unsigned long long*>(a.first_stop), static_cast<unsigned long long>(t));
+    }
 }
 
-// First k in [t, lim) with pred(k), scanning 64 chunks per step (all lanes
-// of the wave call it with the same arguments); lim if none.
-template <class P>
-__device__ __forceinline__ uint64_t wave_find(uint64_t t, uint64_t lim, P pred) {
+// First k in [t, lim) with flag[k] != 0, 64 per ballot (all lanes of the
+// wave call it with the same arguments); lim if none.
+__device__ __forceinline__ uint64_t wave_find(const uint8_t* flag, uint64_t t, uint64_t lim) {
     const int lane = threadIdx.x & 63;
     for (uint64_t b = t; b < lim; b += 64) {
         const uint64_t k = b + lane;
-        const uint64_t m = __ballot(k < lim && pred(k));
+        const uint64_t m = __ballot(k < lim && flag[k] != 0);
         if (m) return b + __ffsll(static_cast<unsigned long long>(m)) - 1;
     }
     return lim;
+}
+
+// The same over a three-level flag hierarchy (chunk, 256 chunks, 65536
+// chunks): at most a few short scans per level.
+__device__ __forceinline__ uint64_t hier_find(const uint8_t* l1, const uint8_t* l2, const uint8_t* l3, uint64_t t,
+                                              uint64_t lim) {
+    if (t >= lim) return lim;
+    const uint64_t e1 = min(lim, (t | 255) + 1);
+    uint64_t k = wave_find(l1, t, e1);
+    if (k < e1) return k;
+    const uint64_t nb = (lim + 255) >> 8;
+    const uint64_t b0 = (t >> 8) + 1;
+    const uint64_t e2 = min(nb, ((t >> 16) + 1) << 8);
+    uint64_t b = wave_find(l2, b0, e2);
+    if (b >= e2) {
+        const uint64_t ns = (lim + 65535) >> 16;
+        const uint64_t sidx = wave_find(l3, (t >> 16) + 1, ns);
+        if (sidx >= ns) return lim;
+        b = wave_find(l2, sidx << 8, min(nb, (sidx + 1) << 8));
+        if (b >= nb) return lim;
+    }
+    return wave_find(l1, b << 8, min(lim, (b + 1) << 8));
 }
 
 // One wave. No-op when every guess was verified, or when the true chain
@@ -187,12 +270,19 @@ __global__ __launch_bounds__(64) void frame_walk_kernel(FrameArgs a) {
     if (s0 != kNone && s0 < f0) return;
     const uint64_t P = a.nchunks;
     uint64_t t = f0, E = a.g[f0];
+#ifdef ONC_FRAME_DEBUG
+    if (lane == 0) printf("frame_walk: P=%lu first_fail=%lu first_stop=%lu g=%lu x=%lu st=%d\n", (unsigned long)P,
+                          (unsigned long)f0, (unsigned long)s0, (unsigned long)E, (unsigned long)a.x[f0], a.st[f0]);
+    uint64_t iters = 0;
+#endif
     for (;;) {
+#ifdef ONC_FRAME_DEBUG
+        ++iters;
+#endif
         const uint64_t g = a.g[t];
         if (g == E && a.fail[t] == 0) {
-            const uint64_t f2 = wave_find(t + 1, P, [&](uint64_t k) { return a.fail[k] != 0; });
-            const uint64_t s2 =
-                wave_find(t, f2, [&](uint64_t k) { return a.g[k] != kNone && a.st[k] != kExit; });
+            const uint64_t f2 = hier_find(a.fail, a.fail2, a.fail3, t + 1, P);
+            const uint64_t s2 = hier_find(a.stop, a.stop2, a.stop3, t, f2);
             if (s2 < f2 || f2 >= P) {
                 if (lane == 0) *a.first_stop = s2 < f2 ? s2 : kNone;
                 break;

@@ -45,7 +45,7 @@ struct IovArgs {
     uint64_t* block_hdr_base;
 };
 
-constexpr uint64_t kFrameChunk = 1024;   // stream bytes per framing lane
+constexpr uint64_t kFrameChunk = 4096;   // stream bytes per framing lane
 
 struct FrameArgs {
     const uint8_t* wire;
@@ -60,7 +60,12 @@ struct FrameArgs {
     uint32_t* cnt;          // records started in the chunk
     int32_t* st;            // -1 = left the chunk, else the stop status
     uint32_t* aux;          // 2 per chunk
-    uint8_t* fail;
+    uint8_t* fail;          // chunk's check failed
+    uint8_t* stop;          // chunk's chain ends in it
+    uint8_t* fail2;         // per 256 chunks
+    uint8_t* stop2;
+    uint8_t* fail3;         // per 65536 chunks
+    uint8_t* stop3;
     uint32_t* cnt_eff;      // records framed from this chunk
     uint64_t* cnt_base;     // exclusive scan of cnt_eff
     uint64_t* first_fail;
