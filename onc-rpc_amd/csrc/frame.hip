@@ -105,54 +105,55 @@ __device__ __forceinline__ uint32_t high_nibble(uint32_t w) {
 }
 
 // First position in [c0, c1) whose bytes look like a record start (a guess:
-// correctness never depends on it). 64 positions per step from an 80-byte
-// register window (five aligned 16-byte loads): a record start has its
-// last-fragment bit set and a message type word of 0 or 1, i.e. three zero
-// bytes at +8..+10; byte masks of the window select the candidates, and only
-// those get the full test.
+// correctness never depends on it). 256 positions per step from a 272-byte
+// register window (seventeen aligned 16-byte loads, all in flight together):
+// a record start has its last-fragment bit set and a message type word of 0
+// or 1, i.e. three zero bytes at +8..+10; byte masks of the window select the
+// candidates, and only those get the full test (plausible_at, twice: the
+// candidate and the start its length points to).
+constexpr int kGuessBlocks = 16;              // 16-byte blocks of positions per step
 __device__ __forceinline__ uint64_t guess_start(const FrameArgs& a, uint64_t c0, uint64_t c1) {
     const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
     const uint64_t lastblk = (a.len - 1) & ~uint64_t(15);   // last 16-byte block holding a buffer byte
-    for (uint64_t blk = c0 & ~uint64_t(15); blk < c1; blk += 64) {
-        uint64_t Z0 = 0, H0 = 0;
-        uint32_t Z1 = 0;
+    const uint64_t hi_pos = min(c1, a.len >= 16 ? a.len - 15 : 0);   // candidates p < hi_pos
+    constexpr int kSub = kGuessBlocks / 4;    // 64-position sub-blocks per step
+    for (uint64_t blk = c0 & ~uint64_t(15); blk < c1; blk += 16 * kGuessBlocks) {
+        uint64_t Z[kSub + 1] = {}, H[kSub] = {};
 #pragma unroll
-        for (int b = 0; b < 5; ++b) {
+        for (int b = 0; b <= kGuessBlocks; ++b) {
             const uint64_t o = blk + 16 * b;
             const u32x4 v = gload<u32x4>(base + (o <= lastblk ? o : lastblk));
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int d = 4 * b + i;
-                if (d < 16) {
-                    Z0 |= uint64_t(zero_nibble(w[i])) << (4 * d);
-                    H0 |= uint64_t(high_nibble(w[i])) << (4 * d);
-                } else {
-                    Z1 |= zero_nibble(w[i]) << (4 * (d - 16));
-                }
+                const int d = 4 * b + i;             // dword index in the window
+                Z[d >> 4] |= uint64_t(zero_nibble(w[i])) << (4 * (d & 15));
+                if (d < 4 * kGuessBlocks) H[d >> 4] |= uint64_t(high_nibble(w[i])) << (4 * (d & 15));
             }
         }
-        // bit k: bytes k+8, k+9, k+10 are zero (80-bit Z = Z1:Z0)
-        const uint64_t z8 = (Z0 >> 8) | (uint64_t(Z1) << 56);
-        const uint64_t z9 = (Z0 >> 9) | (uint64_t(Z1) << 55);
-        const uint64_t z10 = (Z0 >> 10) | (uint64_t(Z1) << 54);
-        uint64_t cand = H0 & z8 & z9 & z10;
-        // positions inside [c0, c1) with 16 bytes of buffer
-        const uint64_t lo = c0 > blk ? c0 - blk : 0;
-        const uint64_t hi_pos = min(c1, a.len >= 16 ? a.len - 15 : 0);   // p < hi_pos
-        const uint64_t hi = hi_pos > blk ? min(uint64_t(64), hi_pos - blk) : 0;
-        cand &= (hi >= 64 ? ~0ull : ((1ull << hi) - 1)) & ~((1ull << lo) - 1);
-        while (cand) {
-            const uint64_t p = blk + __ffsll(static_cast<unsigned long long>(cand)) - 1;
-            if (plausible_at(a, p)) {
-                // and the record it claims is followed by another plausible
-                // start (or the buffer's end): rejects words inside a record
-                // that happen to look like a header (e.g. the xid of a
-                // denied reply, whose next words are 1, 1, 1).
-                const uint64_t q = p + uint64_t(be_at(base, p) & 0x7FFFFFFFu) + 4;
-                if (q + 16 > a.len || plausible_at(a, q)) return p;
+#pragma unroll
+        for (int sb = 0; sb < kSub; ++sb) {
+            const uint64_t sbase = blk + 64 * sb;
+            // bit k: bytes k+8, k+9, k+10 of the sub-block are zero
+            const uint64_t z8 = (Z[sb] >> 8) | (Z[sb + 1] << 56);
+            const uint64_t z9 = (Z[sb] >> 9) | (Z[sb + 1] << 55);
+            const uint64_t z10 = (Z[sb] >> 10) | (Z[sb + 1] << 54);
+            uint64_t cand = H[sb] & z8 & z9 & z10;
+            const uint64_t lo = c0 > sbase ? c0 - sbase : 0;
+            const uint64_t hi = hi_pos > sbase ? min(uint64_t(64), hi_pos - sbase) : 0;
+            cand &= (hi >= 64 ? ~0ull : ((1ull << hi) - 1)) & (lo >= 64 ? 0ull : ~((1ull << lo) - 1));
+            while (cand) {
+                const uint64_t p = sbase + __ffsll(static_cast<unsigned long long>(cand)) - 1;
+                if (plausible_at(a, p)) {
+                    // and the record it claims is followed by another plausible
+                    // start (or the buffer's end): rejects words inside a record
+                    // that happen to look like a header (e.g. the xid of a
+                    // denied reply, whose next words are 1, 1, 1).
+                    const uint64_t q = p + uint64_t(be_at(base, p) & 0x7FFFFFFFu) + 4;
+                    if (q + 16 > a.len || plausible_at(a, q)) return p;
+                }
+                cand &= cand - 1;
             }
-            cand &= cand - 1;
         }
     }
     return kNone;
