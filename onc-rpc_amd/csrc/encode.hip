@@ -11,11 +11,13 @@
 //              per-64-record-tile and per-256-record-workgroup byte totals.
 //   scan       single-workgroup exclusive scan of the workgroup totals.
 //   enc_emit   wave per 64-record tile: wavefront __shfl scan places the
-//              records; headers staged in LDS; the tile's output bytes are
-//              produced in 16-byte chunks, 1 KiB contiguous per wave per step
-//              (global_store_dwordx4). Handles tiles whose records are all
-//              4-byte aligned (every output dword is wholly header or wholly
-//              payload) and whose headers fit LDS; flags the others.
+//              records; the tile's non-pure 16-byte chunks (those holding
+//              header bytes) are assembled in an LDS image; the output is
+//              streamed chunk by chunk, 1 KiB contiguous per wave per step
+//              (global_store_dwordx4): one 16-byte payload load (clamped into
+//              the payload, dword-rotated) + one ds_read_b128 per chunk.
+//              Handles tiles whose records are all 4-byte aligned; flags the
+//              others.
 //   enc_fixup  wave per flagged tile (exits at once for the others): the
 //              byte-general path — header image pre-shifted to each
 //              record's output alignment, payload bytes via clamped dword
@@ -82,53 +84,48 @@ __device__ __forceinline__ uint64_t tile_start(const EncArgs& a, uint64_t tile) 
     return T0;
 }
 
-// ---------------------------------------------------------------------------
-// enc_emit: the hot kernel (word-aligned tiles).
-// ---------------------------------------------------------------------------
-constexpr int kFastHdrCap = 1024;             // header words per span (4 KiB of LDS)
-static_assert(8 * (7 + 2 * 52) <= kFastHdrCap, "a span of 8 maximal headers must fit LDS");
-constexpr int kFastMapCap = 1024;             // output granules per wave tile
-constexpr int kFastWaves = 4;                 // wave tiles per workgroup
-constexpr int kEmitUnroll = 1;                // output chunks per lane per step
+constexpr int kFastMapCap = 1024;             // output granules per wave tile (enc_fixup)
+constexpr int kFastWaves = 4;                 // wave tiles per enc_emit workgroup
 
-// Per-record LDS entry of enc_emit (two ds_read_b128).
-struct FastEnt {
-    uint64_t pst;       // first payload byte
-    uint64_t en;        // one past the last byte
-    uint64_t srcbase;   // payload byte at output offset o lives at srcbase + o
-    int32_t dw;         // LDS header word of the output dword at p: ((p - T0) >> 2) + dw
-    int32_t dwn;        // the same for the next record
+// ---------------------------------------------------------------------------
+// enc_emit (chunk image): word-aligned tiles, every load of a step in flight.
+// ---------------------------------------------------------------------------
+// The span's output is cut into 16-byte chunks. A chunk wholly inside one
+// record's payload is "pure". Every other chunk holds header bytes; its
+// header bytes are assembled in LDS while the wave stages the span, in an
+// image that is the span's output with the pure chunks cut out: chunk c of
+// record r sits at slot c - NP_r before r's pure run and c - NP_r - np_r
+// after it (np_r = r's pure chunks, NP_r = the sum over the records before
+// r). The stream loop then does, per chunk, one 16-byte payload load and
+// one ds_read_b128 of its image slot, and takes each dword from one or the
+// other. The payload load of a chunk that is only partly payload is clamped
+// into the payload ([pst, en - 16]) and its dwords rotated into place, so
+// nothing outside the payload is read and the staging does no payload loads
+// (records with 0 < payload < 16 bytes put their payload in the image).
+// No branch separates one chunk's load from the next, so kU chunks per lane
+// (kU KiB per wave) are in flight at once.
+constexpr int kImgChunks = 248;               // image capacity per span (3968 B: 6 workgroups per CU)
+constexpr int kMap2Cap = 512;                 // granules per span (granule = 4 chunks, doubled to fit)
+constexpr int kEmitChunkUnroll = 1;           // chunks per lane per step (1, 2, 4 measured equal)
+constexpr uint64_t kFastTileMax = 1ull << 30; // larger tiles go to enc_fixup (int32 offsets here)
+// a record's own non-pure chunks: header <= 4 * (7 + 2 * 52) bytes, + the
+// chunk it shares with its predecessor, + its tail chunk
+static_assert((4 * (7 + 2 * 52) + 15) / 16 + 2 <= kImgChunks / 8, "a span of 8 maximal records must fit");
+
+struct ImgTile {
+    uint4 img[kImgChunks];           // assembled non-pure chunks (header bytes; small payloads)
+    int4 ent[kEmitRecs + 1];         // {cf, cp0, cp1, NP} (chunks, span-relative); [ns].x = sentinel
+    int4 pay[kEmitRecs + 1];         // {pst, en (bytes, span-chunk-relative; pst = en: no stream payload), src lo, hi}
+    uint8_t map[kMap2Cap];           // granule -> span record owning its first chunk
 };
 
-struct FastTile {
-    FastEnt ent[kEmitRecs + 1];      // [span records] = sentinel {S1, S1, 0, 0, 0}
-    uint32_t hdr[kFastHdrCap];       // header words of the span's records (stream order)
-    uint8_t map[kFastMapCap];        // granule -> span record holding its first byte
-};
+__device__ __forceinline__ uint32_t sel4(const u32x4_a4& x, uint32_t i) {
+    return i == 0 ? x.x : (i == 1 ? x.y : (i == 2 ? x.z : x.w));
+}
 
-// enc_emit: every wavefront owns one tile of kEmitRecs = 64 records and
-// never waits for another wave (no workgroup barrier), so the staging of one
-// wave overlaps the streaming of the others on the same CU.
-//  Staging (lane per record): plan_record() again (the same function as
-//  enc_len, so lengths agree); one wavefront __shfl scan places output
-//  bytes and LDS header words; each record writes its LDS entry, serialises
-//  its header words into LDS, and claims its output granules in the
-//  granule map (granule = 64 B, doubled until the tile fits the map).
-//  Tiles whose records are not all 4-byte aligned (unpadded odd-length
-//  payloads), or whose headers exceed the LDS budget, are flagged for
-//  enc_fixup in tile_base.
-//  Chunk pass (lane per 16-byte output chunk, 1 KiB contiguous per wave):
-//  granule map -> record entry; a chunk inside its record's payload is one
-//  unaligned 16-byte load; any other chunk takes each of its four dwords
-//  from the LDS header image (this record's or the next one's header) or
-//  the payload. Every chunk of a step, payload-only or not, is stored by the
-//  same global_store_dwordx4, so 128-byte lines are always written whole
-//  (a line left partially written costs a read-modify-write at eviction).
-//  Chunks straddling a tile boundary are written with byte stores of only
-//  this tile's bytes, so tiles never exchange data.
 template <int kU>
 __global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) {
-    __shared__ FastTile s_tiles[kFastWaves];
+    __shared__ ImgTile s_tiles[kFastWaves];
 
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
@@ -136,7 +133,8 @@ __global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) 
     const uint64_t r0 = tile * kEmitRecs;
     if (r0 >= a.n) return;
     const uint64_t T0 = tile_start(a, tile);
-    FastTile& T = s_tiles[wv];
+    ImgTile& T = s_tiles[wv];
+    uint32_t* img32 = reinterpret_cast<uint32_t*>(T.img);
     const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
     const uintptr_t payload = reinterpret_cast<uintptr_t>(a.payload_arena);
 
@@ -151,105 +149,124 @@ __global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) 
         poff = d.payload_off;
         word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((payload + d.payload_off) & 3) == 0);
     }
-    // One wave scan places output bytes and LDS header words: (len << 16 | hw).
-    const uint64_t sv = (len << 16) | hw;
-    const uint64_t incl = wave_incl_scan_u64(sv);
-    const uint64_t excl = incl - sv;
-    const uint64_t start = T0 + (excl >> 16);
+    const uint64_t incl = wave_incl_scan_u64(len);
+    const uint64_t start = T0 + incl - len;
     const uint64_t en = start + len;
     const uint64_t pst = start + 4ull * hw;
-    const uint32_t hoff = uint32_t(excl & 0xFFFFu);
-    const uint32_t hincl = uint32_t(incl & 0xFFFFu);
     if (lane < nrec) {
         a.rec_off[r0 + lane] = start;
         if (len != 0 && en > a.out_cap) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
     }
-    const bool fast = __all(word_aligned) && (T0 & 3) == 0;
+    const bool fast = __all(word_aligned) && (T0 & 3) == 0 && __shfl(incl, 63, 64) < kFastTileMax;
     if (lane == 0) a.tile_base[tile] = T0 | (fast ? 0 : kDeferBit);
     if (!fast) return;
 
-    // Spans: the tile's records in groups of S (64, 32, 16 or 8) whose header
-    // words fit kFastHdrCap (8 records always fit: <= 111 words each).
-    int S = kEmitRecs;
-    for (; S > 8; S >>= 1) {
-        const int g0 = lane & ~(S - 1);
-        const int g1 = min(lane | (S - 1), nrec - 1);
-        const uint32_t top = __shfl(hincl, g1, 64);
-        const uint32_t bot = __shfl(hoff, g0, 64);
-        if (!__any(g0 < nrec && top - bot > uint32_t(kFastHdrCap))) break;
-    }
+    // Absolute chunk indices: owned chunks [cfa, own_next), pure [p0, p1).
+    const int64_t cfa = int64_t((start + 15) >> 4);
+    const int64_t p0 = int64_t((pst + 15) >> 4);
+    const int64_t p1 = max(p0, int64_t(en >> 4));
+    const int64_t np = len ? p1 - p0 : 0;
+    const int64_t cfa_next = __shfl_down(cfa, 1, 64);
+    const int64_t cfa_end = int64_t((__shfl(en, nrec - 1, 64) + 15) >> 4);
+    const int64_t own_next = lane + 1 < nrec ? cfa_next : cfa_end;
+    const uint32_t nonpure = lane < nrec && len ? uint32_t(own_next - cfa - np) : 0u;
+    const uint64_t wnp = wave_incl_scan_u64(nonpure);
+    const uint64_t plen = en - pst;
+
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.msgs);   // >= 64 valid bytes
-    for (int lo_rec = 0; lo_rec < nrec; lo_rec += S) {
-        const int hi_rec = min(nrec, lo_rec + S);
+    int lo_rec = 0;
+    while (lo_rec < nrec) {
+        // span: records [lo_rec, hi_rec) whose non-pure chunks (+1 for a
+        // chunk shared with the record before) fit the image
+        const uint64_t wbase = lo_rec ? __shfl(wnp, lo_rec - 1, 64) : 0;
+        const uint64_t over = __ballot(lane >= lo_rec && lane < nrec && wnp - wbase + 1 > uint64_t(kImgChunks));
+        const int hi_rec = over ? min(nrec, int(__builtin_ctzll(over))) : nrec;
         const int ns = hi_rec - lo_rec;
         const uint64_t S0 = __shfl(start, lo_rec, 64);
         const uint64_t S1 = __shfl(en, hi_rec - 1, 64);
-        const uint32_t hb = __shfl(hoff, lo_rec, 64);
+        const int64_t C0 = int64_t(S0 >> 4);
+        const uint64_t B0 = uint64_t(C0) << 4;        // byte origin of the span-relative offsets
         if (lo_rec) wave_lds_sync();                   // the previous span's readers are done
         const bool active = lane >= lo_rec && lane < hi_rec;
         const int j = lane - lo_rec;
-        const int32_t dw = int32_t(hoff - hb) - int32_t((start - S0) >> 2);
-        const int32_t dwn_raw = __shfl_down(dw, 1, 64);
+        const int64_t npx = active ? np : 0;
+        const int64_t NP = int64_t(wave_incl_scan_u64(uint64_t(npx))) - npx;   // lanes < lo_rec add 0
+        const int32_t NC = int32_t(((S1 + 15) >> 4) - C0);
+        uint32_t gsh = 2;                              // granule = 4 chunks, doubled until the span fits
+        while ((NC >> gsh) >= kMap2Cap) ++gsh;
+        const uint64_t nonempty = __ballot(active && len != 0);
         if (active) {
-            T.ent[j] = FastEnt{pst, en, payload + poff - pst, dw, lane + 1 < hi_rec ? dwn_raw : dw};
+            const bool small = plen != 0 && plen < 16;    // payload kept in the image
+            const uintptr_t sb = payload + poff - pst;    // payload byte at output offset o: sb + o
+            T.ent[j] = make_int4(int32_t(cfa - C0), int32_t(p0 - C0), int32_t(p1 - C0), int32_t(NP));
+            const int32_t ps = int32_t(pst - B0), pe = int32_t(en - B0);
+            T.pay[j] = make_int4(small ? pe : ps, pe, int32_t(uint32_t(sb)), int32_t(uint32_t(sb >> 32)));
             if (len != 0) {
-                // descriptor re-read (L2) rather than kept live across the spans
+                // header words: image dword of output dword P is P - 4 (C0 + NP)
+                const int64_t ib = int64_t(start >> 2) - 4 * (C0 + NP);
                 const onc_msg d = a.msgs[r0 + lane];
                 const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
-                put_header_words(d, uint32_t(len), src, &T.hdr[hoff - hb]);
+                put_header_words(d, uint32_t(len), src, &img32[ib]);
+                if (small) {
+                    // all of it lies in non-pure chunks (np = 0): right after the header
+                    for (uint32_t k = 0; 4 * k < plen; ++k) img32[ib + hw + k] = gload<uint32_t>(sb + pst + 4 * k);
+                }
+                // granules whose first chunk this record owns (chunk 0 of a
+                // span not starting on a chunk: its first non-empty record)
+                const int32_t own_lo = (S0 & 15) && lane == __builtin_ctzll(nonempty) ? 0 : int32_t(cfa - C0);
+                const int32_t own_hi = int32_t(own_next - C0);    // <= NC
+                const int32_t g_hi = min((own_hi + (1 << gsh) - 1) >> gsh, kMap2Cap);
+                for (int32_t g = (own_lo + (1 << gsh) - 1) >> gsh; g < g_hi; ++g) T.map[g] = uint8_t(j);
             }
         }
-        // granule size: 64 B, doubled until the span's bytes fit the map
-        uint32_t gs = 6;
-        while (((S1 - S0) >> gs) >= uint64_t(kFastMapCap)) ++gs;
-        const uint64_t G0 = S0 >> gs;
-        if (active && len != 0) {
-            // claim the granules whose first byte lies in this record
-            const uint64_t gsz = 1ull << gs;
-            for (uint64_t g = (start + gsz - 1) >> gs; g <= (en - 1) >> gs; ++g) T.map[g - G0] = uint8_t(j);
-        }
-        if (lane == 0) {
-            T.ent[ns] = FastEnt{S1, S1, 0, 0, 0};
-            if (S0 & ((1ull << gs) - 1)) T.map[0] = 0;   // granule 0 starts before the span
-        }
+        if (lane == 0) T.ent[ns] = make_int4(0x7FFFFFFF, 0, 0, 0);
         wave_lds_sync();
 
         const uint64_t E = min(S1, a.out_cap);
-        if (E <= S0) continue;                        // no bytes (all records failed, or beyond out_cap)
-        // kU chunks per lane per step: their loads are all in flight before
-        // the first store.
-        const uint64_t cend = (E + 15) >> 4;
-        for (uint64_t c = (S0 >> 4) + lane; c < cend; c += 64 * kU) {
-            uint32_t v[kU][4];
+        lo_rec = hi_rec;
+        if (E <= S0) continue;                         // no bytes (all records failed, or beyond out_cap)
+        const int32_t NCe = int32_t(((E + 15) >> 4) - C0);
+        for (int32_t step = 0; step < NCe; step += 64 * kU) {
+            uintptr_t A[kU];
+            int32_t slot[kU];
+            uint32_t sel[kU];      // bits 0-3: dword i is payload; bits 4-5: rotation
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                const uint64_t o = (c + 64 * u) << 4;
-                const uint64_t lo = max(o, S0);
-                if (c + 64 * u >= cend) break;
-                int r = T.map[(lo >> gs) - G0];
-                FastEnt e = T.ent[r];
-                while (lo >= e.en) e = T.ent[++r];        // sentinel en = S1 > lo
-                if (o >= e.pst && o + 16 <= e.en) {
-                    load16_unaligned(e.srcbase + o, v[u]);
-                } else {
-                    const int64_t q = (int64_t(o) - int64_t(S0)) >> 2;
+                const int32_t c = min(step + lane + 64 * u, NCe - 1);
+                int r = T.map[c >> gsh];
+                while (c >= T.ent[r + 1].x) ++r;
+                const int4 m = T.ent[r];
+                const int4 q = T.pay[r];
+                const int32_t s = c - m.w - (c >= m.z ? m.z - m.y : 0);
+                slot[u] = s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s);
+                const int32_t o = c << 4;
+                const bool hasp = q.x < q.y && o < q.y && o + 16 > q.x;
+                const int32_t x = max(q.x, min(o, q.y - 16));          // clamped window start
+                const uint64_t sbase = uint64_t(uint32_t(q.z)) | (uint64_t(uint32_t(q.w)) << 32);
+                A[u] = hasp ? sbase + B0 + uint64_t(int64_t(x)) : dummy;
+                uint32_t pm = 0;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint64_t p = o + 4 * i;
-                        const bool in_pay = p >= e.pst && p < e.en;
-                        const int64_t hidx = q + i + (p >= e.en ? e.dwn : e.dw);
-                        const int64_t hcl = hidx < 0 ? 0 : (hidx >= kFastHdrCap ? kFastHdrCap - 1 : hidx);
-                        const uint32_t h = T.hdr[hcl];
-                        const uint32_t w = gload<uint32_t>(in_pay ? e.srcbase + p : dummy);
-                        v[u][i] = in_pay ? w : h;
-                    }
-                }
+                for (int i = 0; i < 4; ++i) pm |= (o + 4 * i >= q.x && o + 4 * i < q.y) ? (1u << i) : 0u;
+                sel[u] = (hasp ? pm : 0u) | (uint32_t((o - x) >> 2) & 3u) << 4;
+            }
+            u32x4_a4 X[kU];
+            uint4 L[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                X[u] = gload<u32x4_a4>(A[u]);
+                L[u] = T.img[slot[u]];
             }
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                const uint64_t o = (c + 64 * u) << 4;
-                if (c + 64 * u >= cend) break;
-                store_chunk(a.out, o, max(o, S0), min(o + 16, E), v[u]);
+                const int32_t c = step + lane + 64 * u;
+                if (c >= NCe) break;
+                const uint32_t rot = sel[u] >> 4;
+                const uint32_t h[4] = {L[u].x, L[u].y, L[u].z, L[u].w};
+                uint32_t v[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = (sel[u] >> i) & 1 ? sel4(X[u], (i + rot) & 3) : h[i];
+                const uint64_t o = B0 + (uint64_t(c) << 4);
+                store_chunk(a.out, o, max(o, S0), min(o + 16, E), v);
             }
         }
     }
@@ -424,7 +441,7 @@ hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
 
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
     const uint64_t blocks = (num_emit_tiles(a.n) + kFastWaves - 1) / kFastWaves;
-    hipLaunchKernelGGL((enc_emit_kernel_t<kEmitUnroll>), dim3(uint32_t(blocks)), dim3(64 * kFastWaves), 0, s, a);
+    hipLaunchKernelGGL((enc_emit_kernel_t<kEmitChunkUnroll>), dim3(uint32_t(blocks)), dim3(64 * kFastWaves), 0, s, a);
     return hipGetLastError();
 }
 

@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out
 ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1; rc=$?; echo "pytest rc=$rc"; ok $rc || exit $rc
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?; echo "pytest rc=$rc"; ok $rc || exit $rc
 timeout -k 10 200 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; ok $rc || exit $rc
 timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; rc=$?; echo "bench rc=$rc"; ok $rc || exit $rc
 if [ "${PROFILE:-1}" = "1" ]; then

@@ -42,6 +42,40 @@ __global__ __launch_bounds__(256) void v_copy(const uint4* __restrict__ in, uint
         out[i] = in[i];
 }
 
+// ---- copy variants: U 16-byte loads in flight per lane, optional nontemporal
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void v_copy_u(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n16) {
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n16; i += stride * U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = i + u * stride;
+            if (k < n16) { if (NT) { const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in) + k); v[u] = make_uint4(t.x, t.y, t.z, t.w); } else v[u] = in[k]; }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = i + u * stride;
+            if (k < n16) { if (NT) __builtin_nontemporal_store(u32x4{v[u].x, v[u].y, v[u].z, v[u].w}, reinterpret_cast<u32x4*>(out) + k); else out[k] = v[u]; }
+        }
+    }
+}
+__global__ __launch_bounds__(256) void v_read(const uint4* __restrict__ in, uint64_t n16, uint32_t* sink) {
+    uint32_t acc = 0;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * 256) {
+        const uint4 v = in[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+template <bool NT>
+__global__ __launch_bounds__(256) void v_write(uint4* __restrict__ out, uint64_t n16) {
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * 256) {
+        const uint4 v = make_uint4(uint32_t(i), 1, 2, 3);
+        if (NT) __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(out) + i); else out[i] = v;
+    }
+}
+
 // ---- V_fixed: configs[1]-only structured copy (record = arithmetic) -------
 // Header chunks use the same word logic from registers; measures the cost
 // of the record structure without any LDS/search machinery.
@@ -288,13 +322,21 @@ int main(int argc, char** argv) {
         {"product_len_scan_emit_fixup", true, [&] { launch_enc_len(a2, 0); launch_scan_tiles(a2.block_sum, a2.block_base, num_tiles(n), 0, d_off + n, 0); launch_enc_emit(a2, 0); launch_enc_fixup(a2, 0); }},
         {"product_scan", false, [&] { launch_scan_tiles(a2.block_sum, a2.block_base, num_tiles(n), 0, d_off + n, 0); }},
         {"product_emit_only", false, [&] { launch_enc_emit(a2, 0); }},
-        {"emit_u1", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<1>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"emit_u2", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"emit_u4", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<4>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u1", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<1>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u2", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u4", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<4>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u8", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<8>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
         {"fixup_all_tiles", true, [&] { launch_enc_emit(a2, 0); hipLaunchKernelGGL(flag_all_tiles, dim3(uint32_t((tiles + 255) / 256)), dim3(256), 0, 0, a2.tile_base, tiles); launch_enc_fixup(a2, 0); }},
         {"flag_only", false, [&] { hipLaunchKernelGGL(flag_all_tiles, dim3(uint32_t((tiles + 255) / 256)), dim3(256), 0, 0, a2.tile_base, tiles); }},
         {"copy_256MB_payload_ideal", false,
          [&] { hipLaunchKernelGGL(v_copy, dim3(2048), dim3(256), 0, 0, (const uint4*)d_pay, (uint4*)d_out2, n * P / 16); }},
+        {"copy_u4_2048", false, [&] { hipLaunchKernelGGL((v_copy_u<4, false>), dim3(2048), dim3(256), 0, 0, (const uint4*)d_pay, (uint4*)d_out2, n * P / 16); }},
+        {"copy_u4_nt_2048", false, [&] { hipLaunchKernelGGL((v_copy_u<4, true>), dim3(2048), dim3(256), 0, 0, (const uint4*)d_pay, (uint4*)d_out2, n * P / 16); }},
+        {"copy_u1_8192", false, [&] { hipLaunchKernelGGL((v_copy_u<1, false>), dim3(8192), dim3(256), 0, 0, (const uint4*)d_pay, (uint4*)d_out2, n * P / 16); }},
+        {"copy_u2_nt_4096", false, [&] { hipLaunchKernelGGL((v_copy_u<2, true>), dim3(4096), dim3(256), 0, 0, (const uint4*)d_pay, (uint4*)d_out2, n * P / 16); }},
+        {"read_256MB", false, [&] { hipLaunchKernelGGL(v_read, dim3(4096), dim3(256), 0, 0, (const uint4*)d_pay, n * P / 16, (uint32_t*)d_auth); }},
+        {"write_300MB", false, [&] { hipLaunchKernelGGL((v_write<false>), dim3(4096), dim3(256), 0, 0, (uint4*)d_out2, n * W / 16); }},
+        {"write_300MB_nt", false, [&] { hipLaunchKernelGGL((v_write<true>), dim3(4096), dim3(256), 0, 0, (uint4*)d_out2, n * W / 16); }},
         {"fixed_structured_copy", false,
          [&] { hipLaunchKernelGGL(v_fixed, dim3(2048), dim3(256), 0, 0, d_pay, d_out2, n, W, H); }},
         {"product_len", false, [&] { launch_enc_len(a2, 0); }},
