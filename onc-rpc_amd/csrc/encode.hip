@@ -124,32 +124,27 @@ __device__ __forceinline__ uint32_t sel4(const u32x4_a4& x, uint32_t i) {
 }
 
 template <int kU>
-__global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) {
-    __shared__ ImgTile s_tiles[kFastWaves];
-
+__device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile) {
     const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + wv;
     const uint64_t r0 = tile * kEmitRecs;
-    if (r0 >= a.n) return;
-    const uint64_t T0 = tile_start(a, tile);
-    ImgTile& T = s_tiles[wv];
     uint32_t* img32 = reinterpret_cast<uint32_t*>(T.img);
     const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
     const uintptr_t payload = reinterpret_cast<uintptr_t>(a.payload_arena);
 
+    const uint64_t T0 = tile_start(a, tile);
     uint64_t len = 0, poff = 0;
     uint32_t hw = 0;
     bool word_aligned = true;
     if (lane < nrec) {
         const onc_msg d = a.msgs[r0 + lane];
-        const RecPlan p = plan_record(d, a.unix);
+        const RecPlan p = plan_record(d, a.unix);   // the same function as enc_len: lengths agree
         len = p.len;
         hw = len ? meta_hw(p.meta) : 0;
         poff = d.payload_off;
         word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((payload + d.payload_off) & 3) == 0);
     }
     const uint64_t incl = wave_incl_scan_u64(len);
+    const uint64_t agg = __shfl(incl, 63, 64);
     const uint64_t start = T0 + incl - len;
     const uint64_t en = start + len;
     const uint64_t pst = start + 4ull * hw;
@@ -157,8 +152,17 @@ __global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) 
         a.rec_off[r0 + lane] = start;
         if (len != 0 && en > a.out_cap) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
     }
-    const bool fast = __all(word_aligned) && (T0 & 3) == 0 && __shfl(incl, 63, 64) < kFastTileMax;
-    if (lane == 0) a.tile_base[tile] = T0 | (fast ? 0 : kDeferBit);
+    const bool fast = __all(word_aligned) && (T0 & 3) == 0 && agg < kFastTileMax;
+    if (lane == 0) {
+        a.tile_base[tile] = T0 | (fast ? 0 : kDeferBit);
+        if (!fast) {
+            const uint64_t slot =
+                __hip_atomic_fetch_add(a.ctl + (a.gen & 1), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a.fix_list[slot] = uint32_t(tile);
+        }
+        // the next launch's list counter (its enc_fixup has run before this launch)
+        if (tile == 0) __hip_atomic_store(a.ctl + ((a.gen + 1) & 1), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (!fast) return;
 
     // Absolute chunk indices: owned chunks [cfa, own_next), pure [p0, p1).
@@ -270,6 +274,13 @@ __global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) 
             }
         }
     }
+}
+
+template <int kU>
+__global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) {
+    __shared__ ImgTile s_tiles[kFastWaves];
+    const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
+    if (tile < num_emit_tiles(a.n)) enc_emit_tile<kU>(a, s_tiles[threadIdx.x >> 6], tile);
 }
 
 // ---------------------------------------------------------------------------
@@ -399,12 +410,9 @@ __device__ __forceinline__ void gen_span(GenTile& T, const EncArgs& a, const onc
 
 // enc_fixup: one wavefront (= workgroup) per tile; tiles enc_emit handled
 // exit after reading their flag.
-__global__ __launch_bounds__(64) void enc_fixup_kernel(EncArgs a) {
-    __shared__ GenTile T;
+__device__ __forceinline__ void enc_fixup_tile(const EncArgs& a, GenTile& T, uint64_t tile) {
     const int lane = threadIdx.x;
-    const uint64_t tile = blockIdx.x;
     const uint64_t tb = a.tile_base[tile];
-    if (!(tb & kDeferBit)) return;
     const uint64_t T0 = tb & ~kDeferBit;
     const uint64_t r0 = tile * kEmitRecs;
     const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
@@ -445,9 +453,25 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+constexpr uint32_t kFixupBlocks = 1024;      // persistent: workgroups stride over the flagged tiles
+
+// enc_fixup: one wavefront (= workgroup) per flagged tile, striding over the
+// list enc_emit built (counter ctl[gen & 1]; enc_emit clears the other one
+// for the next launch).
+__global__ __launch_bounds__(64) void enc_fixup_kernel(EncArgs a) {
+    __shared__ GenTile T;
+    const uint64_t count = __hip_atomic_load(a.ctl + (a.gen & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint64_t i = blockIdx.x; i < count; i += gridDim.x) {
+        if (i != blockIdx.x) wave_lds_sync();       // the previous tile's readers are done
+        enc_fixup_tile(a, T, a.fix_list[i]);
+    }
+}
+
 hipError_t launch_enc_fixup(const EncArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(enc_fixup_kernel, dim3(uint32_t(num_emit_tiles(a.n))), dim3(64), 0, s, a);
+    const uint32_t blocks = uint32_t(min(uint64_t(kFixupBlocks), num_emit_tiles(a.n)));
+    hipLaunchKernelGGL(enc_fixup_kernel, dim3(blocks), dim3(64), 0, s, a);
     return hipGetLastError();
 }
+
 
 }  // namespace onc

@@ -25,6 +25,9 @@ struct EncArgs {
     uint64_t* tile_base;    // tiles: byte offset | bit 63 = left to enc_fixup (written by enc_emit)
     uint64_t* block_sum;    // enc_len workgroups (256 records): byte totals
     uint64_t* block_base;   // exclusive scan of block_sum
+    uint64_t* ctl;          // [gen & 1]: tiles enc_emit listed for enc_fixup in launch `gen`
+    uint32_t* fix_list;     // tiles left to enc_fixup
+    uint32_t gen;           // encode launch counter (its parity picks the list counter)
 };
 
 struct IovArgs {
