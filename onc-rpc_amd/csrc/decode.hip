@@ -329,18 +329,27 @@ __global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
             }
         }
         // Header extent from the first round: call -> 36 + cred body + verf
-        // flavor/length + 16 bytes of verifier body; reply -> up to 16 bytes
-        // past an accepted verifier.
+        // flavor/length + the verifier body (its length when the first round
+        // holds it, else a 16-byte guess); reply -> up to 12 bytes past an
+        // accepted verifier.
         const Rd R1{base, q0, 16 * nch, &s_win[t]};
         uint32_t need = uint32_t(min(L, uint64_t(16 * kWinChunks)));
         if (L >= 36 && 16 * nch >= q0 + 36) {
             const uint32_t mt = R1.be32(8);
             if (mt == ONC_MSG_CALL) {
                 const uint32_t cl = R1.be32(32);
-                need = cl <= ONC_MAX_AUTH_LEN ? 36 + cl + pad4(cl) + 8 + 16 : 36;
+                const uint32_t vpos = 36 + cl + pad4(cl) + 4;      // verifier length field
+                if (cl > ONC_MAX_AUTH_LEN) {
+                    need = 36;
+                } else if (q0 + vpos + 4 <= 16 * nch && vpos + 4 <= L) {
+                    const uint32_t vl = R1.be32(vpos);
+                    need = vpos + 4 + (vl <= ONC_MAX_AUTH_LEN ? vl + pad4(vl) : 0);
+                } else {
+                    need = vpos + 4 + 16;
+                }
             } else if (mt == ONC_MSG_REPLY) {
                 const uint32_t vl = R1.be32(20);
-                need = vl <= ONC_MAX_AUTH_LEN ? 24 + vl + pad4(vl) + 16 : 24;
+                need = vl <= ONC_MAX_AUTH_LEN ? 24 + vl + pad4(vl) + 12 : 24;
             }
         }
         const uint32_t want = min(avail, (q0 + need + 15) >> 4);
