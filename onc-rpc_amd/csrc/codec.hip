@@ -326,7 +326,7 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
     // exits at once when there are none).
     rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
-    const uint64_t nblk = onc::num_tiles(batch->n);
+    const uint64_t nblk = onc::num_len_blocks(batch->n);
     rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
         return onc::launch_scan_tiles(a.block_sum, a.block_base, nblk, 0, rec_off + batch->n, c->stream);
     });

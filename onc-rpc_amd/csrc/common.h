@@ -16,6 +16,10 @@ namespace onc {
 constexpr int kTile = 256;        // records per tile (= threads per block)
 constexpr int kScanThreads = 1024;
 constexpr int kEmitRecs = 64;    // records per encode tile = one wavefront (enc_len totals, enc_emit)
+#ifndef ONC_LEN_RECS
+#define ONC_LEN_RECS 1024
+#endif
+constexpr int kLenRecs = ONC_LEN_RECS;   // records per enc_len workgroup (= per scanned total)
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 

@@ -31,11 +31,12 @@ namespace onc {
 constexpr uint64_t kDeferBit = 1ull << 63;   // tile_base flag: tile left to enc_fixup
 
 // Per-record plan + per-tile byte totals: tile = kEmitRecs (64) records =
-// one wavefront (its inclusive __shfl scan, lane 63 writes the total), and
-// per-workgroup totals (kTile = 256 records = 4 tiles) for the scan.
-__global__ __launch_bounds__(kTile) void enc_len_kernel(EncArgs a) {
-    __shared__ uint64_t s_wave[kTile / 64];
-    const uint64_t r = uint64_t(blockIdx.x) * kTile + threadIdx.x;
+// one wavefront scan (lane 63 writes the total); a workgroup of kLenRecs =
+// 1024 lanes (16 waves, one record each) writes its total for the scan.
+__global__ __launch_bounds__(kLenRecs) void enc_len_kernel(EncArgs a) {
+    __shared__ uint64_t s_wave[kLenRecs / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t r = uint64_t(blockIdx.x) * kLenRecs + threadIdx.x;
     uint64_t len = 0;
     if (r < a.n) {
         const onc_msg d = a.msgs[r];
@@ -46,12 +47,16 @@ __global__ __launch_bounds__(kTile) void enc_len_kernel(EncArgs a) {
     }
     const uint64_t incl = wave_incl_scan_u64(len);
     const uint64_t tile = r / kEmitRecs;
-    if ((threadIdx.x & 63) == 63) {
+    if (lane == 63) {
         if (tile * kEmitRecs < a.n) a.tile_sum[tile] = incl;
-        s_wave[threadIdx.x >> 6] = incl;
+        s_wave[wv] = incl;
     }
     __syncthreads();
-    if (threadIdx.x == 0) a.block_sum[blockIdx.x] = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    if (threadIdx.x < 64) {
+        const uint64_t v = threadIdx.x < kLenRecs / 64 ? s_wave[threadIdx.x] : 0;
+        const uint64_t t = wave_incl_scan_u64(v);
+        if (threadIdx.x == 63) a.block_sum[blockIdx.x] = t;
+    }
 }
 
 // LDS writes of one lane become visible to the other lanes of the wave.
@@ -76,12 +81,15 @@ __device__ __forceinline__ void store_chunk(uint8_t* out, uint64_t o, uint64_t l
 }
 
 // Byte offset of tile `tile` in the output: base of its enc_len workgroup
-// (scan of the workgroup totals) + totals of the tiles before it there.
+// (scan of the workgroup totals) + totals of the tiles before it there
+// (lane i loads tile i of the workgroup; one wave reduction). Wave-uniform.
 __device__ __forceinline__ uint64_t tile_start(const EncArgs& a, uint64_t tile) {
-    const uint64_t blk = tile / (kTile / kEmitRecs);
-    uint64_t T0 = a.block_base[blk];
-    for (uint64_t t = blk * (kTile / kEmitRecs); t < tile; ++t) T0 += a.tile_sum[t];
-    return T0;
+    const int lane = threadIdx.x & 63;
+    const uint64_t blk = tile / (kLenRecs / kEmitRecs);
+    const uint64_t t0 = blk * (kLenRecs / kEmitRecs);
+    const uint64_t v = t0 + lane < tile ? a.tile_sum[t0 + lane] : 0;
+    const uint64_t base = a.block_base[blk];
+    return base + __shfl(wave_incl_scan_u64(v), 63, 64);
 }
 
 constexpr int kFastMapCap = 1024;             // output granules per wave tile (enc_fixup)
@@ -106,7 +114,8 @@ constexpr int kFastWaves = 4;                 // wave tiles per enc_emit workgro
 // (kU KiB per wave) are in flight at once.
 constexpr int kImgChunks = 248;               // image capacity per span (3968 B: 6 workgroups per CU)
 constexpr int kMap2Cap = 512;                 // granules per span (granule = 4 chunks, doubled to fit)
-constexpr int kEmitChunkUnroll = 1;           // chunks per lane per step (1, 2, 4 measured equal)
+constexpr int kEmitChunkUnroll = 2;           // chunks per lane per step (2 + nontemporal stores: -5 % vs 1)
+constexpr int kEmitNT = 2;                    // nontemporal output stores (loads: measured slower)
 constexpr uint64_t kFastTileMax = 1ull << 30; // larger tiles go to enc_fixup (int32 offsets here)
 // a record's own non-pure chunks: header <= 4 * (7 + 2 * 52) bytes, + the
 // chunk it shares with its predecessor, + its tail chunk
@@ -123,7 +132,7 @@ __device__ __forceinline__ uint32_t sel4(const u32x4_a4& x, uint32_t i) {
     return i == 0 ? x.x : (i == 1 ? x.y : (i == 2 ? x.z : x.w));
 }
 
-template <int kU>
+template <int kU, int kNT>
 __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = tile * kEmitRecs;
@@ -257,7 +266,8 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
             uint4 L[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                X[u] = gload<u32x4_a4>(A[u]);
+                if (kNT & 1) X[u] = __builtin_nontemporal_load(reinterpret_cast<const ONC_GLOBAL u32x4_a4*>(A[u]));
+                else X[u] = gload<u32x4_a4>(A[u]);
                 L[u] = T.img[slot[u]];
             }
 #pragma unroll
@@ -270,17 +280,22 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
 #pragma unroll
                 for (int i = 0; i < 4; ++i) v[i] = (sel[u] >> i) & 1 ? sel4(X[u], (i + rot) & 3) : h[i];
                 const uint64_t o = B0 + (uint64_t(c) << 4);
-                store_chunk(a.out, o, max(o, S0), min(o + 16, E), v);
+                if ((kNT & 2) && o >= S0 && o + 16 <= E)
+                    __builtin_nontemporal_store(u32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<u32x4*>(a.out + o));
+                else
+                    store_chunk(a.out, o, max(o, S0), min(o + 16, E), v);
             }
         }
     }
 }
 
-template <int kU>
-__global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) {
+// kNT: bit 0 = nontemporal payload loads, bit 1 = nontemporal stores;
+// kOcc: workgroups per CU the register allocation must allow (0 = free)
+template <int kU, int kNT = 0, int kOcc = 0>
+__global__ __launch_bounds__(64 * kFastWaves, kOcc ? kOcc * kFastWaves / 4 : 1) void enc_emit_kernel_t(EncArgs a) {
     __shared__ ImgTile s_tiles[kFastWaves];
     const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
-    if (tile < num_emit_tiles(a.n)) enc_emit_tile<kU>(a, s_tiles[threadIdx.x >> 6], tile);
+    if (tile < num_emit_tiles(a.n)) enc_emit_tile<kU, kNT>(a, s_tiles[threadIdx.x >> 6], tile);
 }
 
 // ---------------------------------------------------------------------------
@@ -442,14 +457,13 @@ __device__ __forceinline__ void enc_fixup_tile(const EncArgs& a, GenTile& T, uin
 }
 
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
-    const uint64_t tiles = num_tiles(a.n);
-    hipLaunchKernelGGL(enc_len_kernel, dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
+    hipLaunchKernelGGL(enc_len_kernel, dim3(uint32_t(num_len_blocks(a.n))), dim3(kLenRecs), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
     const uint64_t blocks = (num_emit_tiles(a.n) + kFastWaves - 1) / kFastWaves;
-    hipLaunchKernelGGL((enc_emit_kernel_t<kEmitChunkUnroll>), dim3(uint32_t(blocks)), dim3(64 * kFastWaves), 0, s, a);
+    hipLaunchKernelGGL((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT>), dim3(uint32_t(blocks)), dim3(64 * kFastWaves), 0, s, a);
     return hipGetLastError();
 }
 

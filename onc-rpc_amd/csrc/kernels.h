@@ -102,6 +102,7 @@ hipError_t launch_len_apply(const uint32_t* len, uint64_t n, const uint64_t* til
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s);
 
 __host__ __device__ inline uint64_t num_tiles(uint64_t n) { return (n + 255) / 256; }
+__host__ __device__ inline uint64_t num_len_blocks(uint64_t n) { return (n + kLenRecs - 1) / kLenRecs; }
 __host__ __device__ inline uint64_t num_emit_tiles(uint64_t n) { return (n + kEmitRecs - 1) / kEmitRecs; }
 
 }  // namespace onc

@@ -10,40 +10,58 @@
 
 namespace onc {
 
-// Exclusive scan of `count` u64 totals by one 1024-thread workgroup. Each
-// thread owns a contiguous segment and reads it in batches of 8 independent
-// loads (one memory latency per batch, not per element); the per-thread
-// sums are combined by the wavefront __shfl + LDS block scan.
+// Exclusive scan of `count` u64 totals by one 1024-thread workgroup, in
+// rows of 1024 x 16 values: each thread loads its 16 contiguous values of
+// the row at once (8 dwordx4, 128 contiguous bytes per lane), keeps them in
+// registers, and the per-thread sums go through the wavefront __shfl + LDS
+// block scan; one memory latency per row (one row covers 16K workgroup
+// totals = 16M records at 1024 records per enc_len workgroup).
+constexpr int kScanPer = 16;
 __global__ __launch_bounds__(kScanThreads) void scan_tiles_kernel(const uint64_t* in, uint64_t* out,
                                                                     uint64_t count, uint64_t base,
                                                                     uint64_t* total_out) {
     __shared__ uint64_t s_wave[kScanThreads / 64];
-    constexpr int kB = 8;
-    const uint64_t per = (count + kScanThreads - 1) / kScanThreads;
-    const uint64_t lo = min(count, uint64_t(threadIdx.x) * per);
-    const uint64_t hi = min(count, lo + per);
-    uint64_t sum = 0;
-    for (uint64_t j = lo; j < hi; j += kB) {
-        uint64_t v[kB];
+    uint64_t carry = base;
+    const bool vec = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+    for (uint64_t row = 0; row < count; row += uint64_t(kScanThreads) * kScanPer) {
+        const uint64_t lo = row + uint64_t(threadIdx.x) * kScanPer;
+        uint64_t v[kScanPer];
+        if (vec && lo + kScanPer <= count) {
+            const ulonglong2* src = reinterpret_cast<const ulonglong2*>(in + lo);
 #pragma unroll
-        for (int k = 0; k < kB; ++k) v[k] = j + k < hi ? in[j + k] : 0;
+            for (int k = 0; k < kScanPer / 2; ++k) {
+                const ulonglong2 w = src[k];
+                v[2 * k] = w.x;
+                v[2 * k + 1] = w.y;
+            }
+        } else {
 #pragma unroll
-        for (int k = 0; k < kB; ++k) sum += v[k];
-    }
-    uint64_t total;
-    const uint64_t excl = block_excl_scan_u64<kScanThreads>(sum, s_wave, &total);
-    uint64_t run = base + excl;
-    for (uint64_t j = lo; j < hi; j += kB) {
-        uint64_t v[kB];
-#pragma unroll
-        for (int k = 0; k < kB; ++k) v[k] = j + k < hi ? in[j + k] : 0;
-#pragma unroll
-        for (int k = 0; k < kB; ++k) {
-            if (j + k < hi) out[j + k] = run;
-            run += v[k];
+            for (int k = 0; k < kScanPer; ++k) v[k] = lo + k < count ? in[lo + k] : 0;
         }
+        uint64_t sum = 0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) sum += v[k];
+        uint64_t total;
+        uint64_t run = carry + block_excl_scan_u64<kScanThreads>(sum, s_wave, &total);
+        if (vec && lo + kScanPer <= count) {
+            ulonglong2* dst = reinterpret_cast<ulonglong2*>(out + lo);
+#pragma unroll
+            for (int k = 0; k < kScanPer / 2; ++k) {
+                const uint64_t r0 = run;
+                run += v[2 * k];
+                dst[k] = make_ulonglong2(r0, run);
+                run += v[2 * k + 1];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kScanPer; ++k) {
+                if (lo + k < count) out[lo + k] = run;
+                run += v[k];
+            }
+        }
+        carry += total;
     }
-    if (threadIdx.x == 0 && total_out) *total_out = base + total;
+    if (threadIdx.x == 0 && total_out) *total_out = carry;
 }
 
 __global__ __launch_bounds__(kTile) void len_tiles_kernel(const uint32_t* len, uint64_t n, uint64_t* tile_sum) {

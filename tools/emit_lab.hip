@@ -60,6 +60,25 @@ __global__ __launch_bounds__(256) void v_copy_u(const uint4* __restrict__ in, ui
         }
     }
 }
+// copy whose source is 4-aligned but not 16-aligned (single a4 dwordx4 load)
+template <int U>
+__global__ __launch_bounds__(256) void v_copy_a4(const uint8_t* __restrict__ in, uint4* __restrict__ out, uint64_t n16, uint32_t shift) {
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    const uintptr_t src = reinterpret_cast<uintptr_t>(in) + shift;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n16; i += stride * U) {
+        u32x4_a4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = i + u * stride;
+            if (k < n16) v[u] = gload<u32x4_a4>(src + 16 * k);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = i + u * stride;
+            if (k < n16) out[k] = make_uint4(v[u].x, v[u].y, v[u].z, v[u].w);
+        }
+    }
+}
 __global__ __launch_bounds__(256) void v_read(const uint4* __restrict__ in, uint64_t n16, uint32_t* sink) {
     uint32_t acc = 0;
     for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * 256) {
@@ -294,7 +313,7 @@ int main(int argc, char** argv) {
     a.fix_list = reinterpret_cast<uint32_t*>(a.ctl + 8);
     a.gen = 1;
     CK(launch_enc_len(a, 0));
-    CK(launch_scan_tiles(a.block_sum, a.block_base, num_tiles(n), 0, d_off + n, 0));
+    CK(launch_scan_tiles(a.block_sum, a.block_base, num_len_blocks(n), 0, d_off + n, 0));
     CK(launch_enc_emit(a, 0));
     CK(launch_enc_fixup(a, 0));
     CK(hipDeviceSynchronize());
@@ -325,10 +344,18 @@ int main(int argc, char** argv) {
     a2.out = d_out2;
     const uint64_t n16 = (n * W + 15) / 16;
     std::vector<Var> vars = {
-        {"product_len_scan_emit_fixup", true, [&] { ++a2.gen; launch_enc_len(a2, 0); launch_scan_tiles(a2.block_sum, a2.block_base, num_tiles(n), 0, d_off + n, 0); launch_enc_emit(a2, 0); launch_enc_fixup(a2, 0); }},
+        {"product_len_scan_emit_fixup", true, [&] { ++a2.gen; launch_enc_len(a2, 0); launch_scan_tiles(a2.block_sum, a2.block_base, num_len_blocks(n), 0, d_off + n, 0); launch_enc_emit(a2, 0); launch_enc_fixup(a2, 0); }},
         {"product_fixup_empty", false, [&] { launch_enc_fixup(a2, 0); }},
         {"product_emit_only", false, [&] { ++a2.gen; launch_enc_emit(a2, 0); }},
         {"img_u1", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<1>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u1_ntld", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<1, 1>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u1_ntst", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<1, 2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u1_ntboth", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<1, 3>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u2_ntboth", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<2, 3>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u1_occ6", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<1, 0, 6>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u2_nt_occ6", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<2, 3, 6>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u2_ntst", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<2, 2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u4_ntboth", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<4, 3>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
         {"img_u2", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
         {"img_u4", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<4>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
         {"img_u8", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<8>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
@@ -340,13 +367,16 @@ int main(int argc, char** argv) {
         {"copy_u4_nt_2048", false, [&] { hipLaunchKernelGGL((v_copy_u<4, true>), dim3(2048), dim3(256), 0, 0, (const uint4*)d_pay, (uint4*)d_out2, n * P / 16); }},
         {"copy_u1_8192", false, [&] { hipLaunchKernelGGL((v_copy_u<1, false>), dim3(8192), dim3(256), 0, 0, (const uint4*)d_pay, (uint4*)d_out2, n * P / 16); }},
         {"copy_u2_nt_4096", false, [&] { hipLaunchKernelGGL((v_copy_u<2, true>), dim3(4096), dim3(256), 0, 0, (const uint4*)d_pay, (uint4*)d_out2, n * P / 16); }},
+        {"copy_a4_shift0_8192", false, [&] { hipLaunchKernelGGL((v_copy_a4<1>), dim3(8192), dim3(256), 0, 0, d_pay, (uint4*)d_out2, n * P / 16 - 1, 0u); }},
+        {"copy_a4_shift4_8192", false, [&] { hipLaunchKernelGGL((v_copy_a4<1>), dim3(8192), dim3(256), 0, 0, d_pay, (uint4*)d_out2, n * P / 16 - 1, 4u); }},
+        {"copy_a4_shift4_u2_4096", false, [&] { hipLaunchKernelGGL((v_copy_a4<2>), dim3(4096), dim3(256), 0, 0, d_pay, (uint4*)d_out2, n * P / 16 - 1, 4u); }},
         {"read_256MB", false, [&] { hipLaunchKernelGGL(v_read, dim3(4096), dim3(256), 0, 0, (const uint4*)d_pay, n * P / 16, (uint32_t*)d_auth); }},
         {"write_300MB", false, [&] { hipLaunchKernelGGL((v_write<false>), dim3(4096), dim3(256), 0, 0, (uint4*)d_out2, n * W / 16); }},
         {"write_300MB_nt", false, [&] { hipLaunchKernelGGL((v_write<true>), dim3(4096), dim3(256), 0, 0, (uint4*)d_out2, n * W / 16); }},
         {"fixed_structured_copy", false,
          [&] { hipLaunchKernelGGL(v_fixed, dim3(2048), dim3(256), 0, 0, d_pay, d_out2, n, W, H); }},
         {"product_len", false, [&] { launch_enc_len(a2, 0); }},
-        {"product_scan", false, [&] { launch_scan_tiles(a2.block_sum, a2.block_base, num_tiles(n), 0, d_off + n, 0); }},
+        {"product_scan", false, [&] { launch_scan_tiles(a2.block_sum, a2.block_base, num_len_blocks(n), 0, d_off + n, 0); }},
         {"lds_lookup_copy_4w", false, [&] { hipLaunchKernelGGL(v_lds<4>, dim3((tiles + 3) / 4), dim3(256), 0, 0, d_pay, d_out2, n, W, H); }},
         
         
