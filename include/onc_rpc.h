@@ -249,7 +249,7 @@ int onc_abi_version(void);
 #define ONC_K_DEC_PARSE   3
 #define ONC_K_LEN_TILES   4
 #define ONC_K_LEN_APPLY   5
-#define ONC_K_ENC_FIXUP   6
+#define ONC_K_ENC_FIXUP   6   /* retired: enc_emit handles every tile; never launched */
 #define ONC_K_IOV_LEN     7
 #define ONC_K_IOV_EMIT    8
 #define ONC_K_FRAME       9

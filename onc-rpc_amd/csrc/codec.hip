@@ -18,7 +18,6 @@ struct onc_codec {
     // scratch (u64 words): [tile_sum | tile_base | block_sum | block_base]
     uint64_t* scratch = nullptr;
     uint64_t scratch_tiles = 0;
-    uint32_t gen = 0;      // encode launch counter (enc_fixup list parity)
     uint8_t* frame_scratch = nullptr;   // onc_frame_stream per-chunk state
     uint64_t frame_chunks = 0;
     uint32_t timing = 0;   // bitmask of ONC_K_* ids whose launches are bracketed
@@ -72,10 +71,8 @@ int run(onc_codec* c, int kernel, const char* what, F&& launch) {
     return ONC_RC_OK;
 }
 
-// scratch (u64 words): [tile_sum T | tile_base T | spare T | block_sum B |
-// block_base B | 16 | ctl 8 | fix_list T u32]
-uint64_t ctl_word(uint64_t T) { return 3 * T + 2 * (T / 4 + 1) + 16; }
-uint64_t scratch_words(uint64_t T) { return ctl_word(T) + 8 + (T + 1) / 2; }
+// scratch (u64 words): [tile_sum T | spare 2T | block_sum B | block_base B | 16]
+uint64_t scratch_words(uint64_t T) { return 3 * T + 2 * (T / 4 + 1) + 16; }
 
 int ensure_scratch(onc_codec* c, uint64_t tiles) {
     if (tiles <= c->scratch_tiles) return ONC_RC_OK;
@@ -94,10 +91,6 @@ int ensure_scratch(onc_codec* c, uint64_t tiles) {
         return ONC_RC_ENOMEM;
     }
     c->scratch_tiles = want;
-    // the enc_fixup list counters
-    e = hipMemsetAsync(c->scratch + ctl_word(want), 0, 8 * sizeof(uint64_t), c->stream);
-    if (e != hipSuccess) return fail(c, e, "hipMemsetAsync(scratch)");
-    c->gen = 0;
     return ONC_RC_OK;
 }
 
@@ -106,18 +99,8 @@ void bind_scratch(onc_codec* c, onc::EncArgs& a) {
     const uint64_t T = c->scratch_tiles;
     const uint64_t B = T / 4 + 1;
     a.tile_sum = c->scratch;
-    a.tile_base = c->scratch + T;
     a.block_sum = c->scratch + 3 * T;
     a.block_base = c->scratch + 3 * T + B;
-    a.ctl = c->scratch + ctl_word(T);
-    a.fix_list = reinterpret_cast<uint32_t*>(a.ctl + 8);
-}
-
-// Next encode launch number (the counter enc_emit clears for the next
-// launch is picked by its parity).
-int next_gen(onc_codec* c, uint32_t* gen) {
-    *gen = ++c->gen;
-    return ONC_RC_OK;
 }
 
 int set_device(onc_codec* c) {
@@ -219,7 +202,7 @@ const char* onc_kernel_name(int k) {
         case ONC_K_DEC_PARSE: return "decode_kernel";
         case ONC_K_LEN_TILES: return "len_tiles_kernel";
         case ONC_K_LEN_APPLY: return "len_apply_kernel";
-        case ONC_K_ENC_FIXUP: return "enc_fixup_kernel";
+        case ONC_K_ENC_FIXUP: return "enc_fixup_kernel (retired)";
         case ONC_K_IOV_LEN: return "iov_len_kernel";
         case ONC_K_IOV_EMIT: return "iov_emit_kernel";
         case ONC_K_FRAME: return "frame_chunks_kernel";
@@ -318,12 +301,8 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
     a.status = status;
     a.rec_len = rec_len;
     bind_scratch(c, a);
-    rc = next_gen(c, &a.gen);
-    if (rc != ONC_RC_OK) return rc;
     // enc_len: plans + tile/workgroup totals; scan: workgroup bases (and the
-    // grand total into rec_off[n]); enc_emit: bytes of word-aligned tiles;
-    // enc_fixup: the tiles enc_emit listed (a short persistent grid that
-    // exits at once when there are none).
+    // grand total into rec_off[n]); enc_emit: the bytes.
     rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
     const uint64_t nblk = onc::num_len_blocks(batch->n);
@@ -331,9 +310,7 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
         return onc::launch_scan_tiles(a.block_sum, a.block_base, nblk, 0, rec_off + batch->n, c->stream);
     });
     if (rc != ONC_RC_OK) return rc;
-    rc = run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
-    if (rc != ONC_RC_OK) return rc;
-    return run(c, ONC_K_ENC_FIXUP, "enc_fixup", [&] { return onc::launch_enc_fixup(a, c->stream); });
+    return run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
 }
 
 int onc_encode_iov(onc_codec* c, const onc_batch* batch, uint8_t* hdr_out, uint64_t hdr_cap, onc_iov_rec* iov,

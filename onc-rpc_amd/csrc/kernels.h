@@ -22,12 +22,8 @@ struct EncArgs {
     int32_t* status;        // n
     uint32_t* rec_len;      // n, optional
     uint64_t* tile_sum;     // tiles
-    uint64_t* tile_base;    // tiles: byte offset | bit 63 = left to enc_fixup (written by enc_emit)
-    uint64_t* block_sum;    // enc_len workgroups (256 records): byte totals
+    uint64_t* block_sum;    // enc_len workgroups (kLenRecs records): byte totals
     uint64_t* block_base;   // exclusive scan of block_sum
-    uint64_t* ctl;          // [gen & 1]: tiles enc_emit listed for enc_fixup in launch `gen`
-    uint32_t* fix_list;     // tiles left to enc_fixup
-    uint32_t gen;           // encode launch counter (its parity picks the list counter)
 };
 
 struct IovArgs {
@@ -85,7 +81,6 @@ struct DecArgs {
 // encode.hip
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s);
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s);
-hipError_t launch_enc_fixup(const EncArgs& a, hipStream_t s);
 // iov.hip
 hipError_t launch_iov_len(const IovArgs& a, hipStream_t s);
 hipError_t launch_iov_emit(const IovArgs& a, hipStream_t s);

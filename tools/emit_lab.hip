@@ -247,16 +247,9 @@ __global__ __launch_bounds__(256) void v_fixed_persist(const uint8_t* __restrict
     }
 }
 
-// flags every tile for enc_fixup (times the byte-general path on the whole batch)
-__global__ void flag_all_tiles(uint64_t* tile_base, uint32_t* fix_list, uint64_t* ctl, uint64_t tiles) {
-    const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (t < tiles) { tile_base[t] |= 1ull << 63; fix_list[t] = uint32_t(t); }
-    if (t == 0) ctl[0] = ctl[1] = tiles;
-}
-
 int main(int argc, char** argv) {
     const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1000000;
-    const uint32_t P = 256, H = 44, W = H + P;
+    const uint32_t P = argc > 2 ? uint32_t(strtoul(argv[2], nullptr, 10)) : 256, H = 44, W = H + P;
     std::vector<onc_msg> msgs(n);
     for (uint64_t i = 0; i < n; ++i) {
         onc_msg& m = msgs[i];
@@ -288,9 +281,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d_auth, 64));
     CK(hipMalloc(&d_unix, sizeof(onc_unix_params)));
     CK(hipMalloc(&d_off, (n + 1) * 8));
-    const uint64_t lbw = 3 * tiles + 2 * (tiles / 4 + 1) + 16;
-    CK(hipMalloc(&d_scr, (lbw + 8 + tiles) * 8));
-    CK(hipMemset(d_scr, 0, (lbw + 8 + tiles) * 8));
+    CK(hipMalloc(&d_scr, (3 * tiles + 2 * (tiles / 4 + 1) + 16) * 8));
     CK(hipMalloc(&d_st, n * 4));
     CK(hipMemcpy(d_msgs, msgs.data(), n * sizeof(onc_msg), hipMemcpyHostToDevice));
     CK(hipMemcpy(d_pay, pay.data(), pay.size(), hipMemcpyHostToDevice));
@@ -306,16 +297,11 @@ int main(int argc, char** argv) {
     a.rec_off = d_off;
     a.status = d_st;
     a.tile_sum = d_scr;
-    a.tile_base = d_scr + tiles;
     a.block_sum = d_scr + 3 * tiles;
     a.block_base = d_scr + 3 * tiles + tiles / 4 + 1;
-    a.ctl = d_scr + lbw;
-    a.fix_list = reinterpret_cast<uint32_t*>(a.ctl + 8);
-    a.gen = 1;
     CK(launch_enc_len(a, 0));
     CK(launch_scan_tiles(a.block_sum, a.block_base, num_len_blocks(n), 0, d_off + n, 0));
     CK(launch_enc_emit(a, 0));
-    CK(launch_enc_fixup(a, 0));
     CK(hipDeviceSynchronize());
     // independent host reference of the configs[1] wire: 11 header words + payload
     std::vector<uint8_t> ref(n * W);
@@ -344,22 +330,20 @@ int main(int argc, char** argv) {
     a2.out = d_out2;
     const uint64_t n16 = (n * W + 15) / 16;
     std::vector<Var> vars = {
-        {"product_len_scan_emit_fixup", true, [&] { ++a2.gen; launch_enc_len(a2, 0); launch_scan_tiles(a2.block_sum, a2.block_base, num_len_blocks(n), 0, d_off + n, 0); launch_enc_emit(a2, 0); launch_enc_fixup(a2, 0); }},
-        {"product_fixup_empty", false, [&] { launch_enc_fixup(a2, 0); }},
-        {"product_emit_only", false, [&] { ++a2.gen; launch_enc_emit(a2, 0); }},
-        {"img_u1", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<1>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u1_ntld", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<1, 1>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u1_ntst", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<1, 2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u1_ntboth", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<1, 3>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u2_ntboth", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<2, 3>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u1_occ6", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<1, 0, 6>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u2_nt_occ6", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<2, 3, 6>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u2_ntst", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<2, 2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u4_ntboth", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<4, 3>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u2", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u4", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<4>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u8", true, [&] { ++a2.gen; hipLaunchKernelGGL((enc_emit_kernel_t<8>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"fixup_all_tiles", true, [&] { ++a2.gen; launch_enc_emit(a2, 0); hipLaunchKernelGGL(flag_all_tiles, dim3(uint32_t((tiles + 255) / 256)), dim3(256), 0, 0, a2.tile_base, a2.fix_list, a2.ctl, tiles); launch_enc_fixup(a2, 0); }},
+        {"product_len_scan_emit", true, [&] { launch_enc_len(a2, 0); launch_scan_tiles(a2.block_sum, a2.block_base, num_len_blocks(n), 0, d_off + n, 0); launch_enc_emit(a2, 0); }},
+        {"product_emit_only", false, [&] { launch_enc_emit(a2, 0); }},
+        {"img_u1", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<1>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u1_ntld", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<1, 1>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u1_ntst", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<1, 2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u1_ntboth", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<1, 3>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u2_ntboth", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<2, 3>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u1_occ6", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<1, 0, 6>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u2_nt_occ6", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<2, 3, 6>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u2_ntst", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<2, 2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u4_ntboth", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<4, 3>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u2", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u4", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<4>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u8", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<8>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
         
         {"copy_256MB_payload_ideal", false,
          [&] { hipLaunchKernelGGL(v_copy, dim3(2048), dim3(256), 0, 0, (const uint4*)d_pay, (uint4*)d_out2, n * P / 16); }},
