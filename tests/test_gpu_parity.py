@@ -237,6 +237,37 @@ def test_write_zero_capacity(codec, R, oracle):
         gpu_vs_oracle_encode(R, codec, oracle, hb, out_cap=cap)
 
 
+@pytest.mark.parametrize("plen", [1023, 1021, 1022])
+def test_byte_path_with_spans(codec, R, oracle, plen):
+    """AUTH_UNIX (16 gids) headers + odd payloads: every tile takes enc_emit's
+    byte path and is cut into several LDS spans."""
+    hb = S.call_unix16(700, plen)
+    gpu_vs_oracle_encode(R, codec, oracle, hb)
+    total = int(oracle.encode_batch(hb)[1][-1])
+    for cap in (total // 2 + 7, total - 3):
+        gpu_vs_oracle_encode(R, codec, oracle, hb, out_cap=cap)
+
+
+def test_small_payload_lengths(codec, R, oracle):
+    """Payloads of 0..40 bytes (those under 16 live in the LDS image), at every
+    record alignment, mixed with AUTH_NONE and AUTH_UNIX headers."""
+    msgs = []
+    rng = np.random.default_rng(5)
+    for i in range(1500):
+        m = S.random_messages(1, seed=1000 + i, max_payload=1)[0]
+        msgs.append(m)
+    hb = L.build_batch(msgs)
+    pl = rng.integers(0, 41, len(hb.msgs)).astype(np.uint32)
+    is_pay = (hb.msgs["msg_type"] == L.MSG_CALL) | \
+        ((hb.msgs["reply_stat"] == L.REPLY_ACCEPTED) & (hb.msgs["stat"] == 0))
+    pay = rng.integers(0, 256, int(pl.sum()) + 64, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(pl)[:-1]]).astype(np.uint64)
+    msgs2 = hb.msgs.copy()
+    msgs2["payload_len"] = np.where(is_pay, pl, msgs2["payload_len"])
+    msgs2["payload_off"] = np.where(is_pay, offs, msgs2["payload_off"])
+    gpu_vs_oracle_encode(R, codec, oracle, L.HostBatch(msgs2, hb.unix, hb.auth_arena, pay))
+
+
 def test_unaligned_arenas(codec, R, oracle):
     """Payload/auth bodies at every byte alignment in the arenas."""
     base = L.build_batch(S.random_messages(600, seed=41, max_payload=70))
