@@ -53,7 +53,9 @@ def parse():
     ap.add_argument("--pcie-reps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="per-kernel PMC traffic (default profiles/traffic_r01.json for c1, "
+                         "profiles/traffic_r01_<workload>.json otherwise)")
     return ap.parse_args()
 
 
@@ -372,7 +374,9 @@ def main():
     achieved = alg / (dom_us * 1e-6) / 1e9
     traffic = None
     try:
-        with open(args.traffic_json) as f:
+        tpath = args.traffic_json or os.path.join(
+            ROOT, "profiles", "traffic_r01.json" if wl == "c1" else f"traffic_r01_{wl}.json")
+        with open(tpath) as f:
             tj = json.load(f)
         if tj.get("records") == n and tj.get("workload_id", "c1") == wl and dom in tj.get("kernels", {}):
             traffic = tj["kernels"][dom]["hbm_bytes_per_launch"]

@@ -207,7 +207,9 @@ typedef struct onc_batch {
  * Offsets in the decoded descriptors are wire-buffer offsets, so a decoded
  * batch can be re-encoded with auth_arena = payload_arena = wire.
  * For a record with status != ONC_OK the descriptor is all zero; unix slots
- * are defined only for OK records whose auth kind is UNIX. */
+ * are defined only for OK records whose auth kind is UNIX (the decoder may
+ * zero the other bytes of a record's 192-byte slot pair, to write whole
+ * 64-byte sectors). */
 typedef struct onc_decoded {
     onc_msg*         msgs;        /* n */
     onc_unix_params* unix_params; /* 2n */

@@ -65,20 +65,36 @@ struct Rules {
 };
 
 // One decoded AUTH_UNIX parameter slot, written with six dwordx4 stores.
+// A record's two slots are 192 bytes = three 64-byte sectors; one slot alone
+// would leave the middle sector half written (a read-modify-write in the
+// memory controller), so the slot is padded to whole sectors with 32 zero
+// bytes of the record's other slot, which is unspecified unless it holds an
+// AUTH_UNIX verifier (written after the credential, so it wins).
+//   pad: 1 = credential slot (zeros after it), 2 = verifier slot whose
+//   credential slot is unused (zeros before it), 0 = no padding.
 __device__ __forceinline__ void put_unix(onc_unix_params* u, uint32_t stamp, uint32_t uid, uint32_t gid,
-                                         uint32_t ng, uint64_t name_off, uint32_t nl, const uint32_t* gids) {
+                                         uint32_t ng, uint64_t name_off, uint32_t nl, const uint32_t* gids,
+                                         uint32_t pad) {
     uint4* d = reinterpret_cast<uint4*>(u);
+    if (pad == 2) {
+        d[-2] = make_uint4(0, 0, 0, 0);
+        d[-1] = make_uint4(0, 0, 0, 0);
+    }
     d[0] = make_uint4(stamp, uid, gid, ng);
     d[1] = make_uint4(uint32_t(name_off), uint32_t(name_off >> 32), nl, 0u);
 #pragma unroll
     for (int k = 0; k < 4; ++k) d[2 + k] = make_uint4(gids[4 * k], gids[4 * k + 1], gids[4 * k + 2], gids[4 * k + 3]);
+    if (pad == 1) {
+        d[6] = make_uint4(0, 0, 0, 0);
+        d[7] = make_uint4(0, 0, 0, 0);
+    }
 }
 
 // Slice mode AuthFlavor::from_cursor (flavor.rs:52-94) with
 // AuthUnixParams::from_cursor (unix_params.rs:90-129) and
 // Opaque::from_wire (opaque.rs:72-98; bound = the whole message, `end`).
 __device__ __forceinline__ int32_t auth_slice(const Rd& R, uint32_t& pos, uint32_t end, uint64_t rec_off,
-                                              uint64_t slot, onc_auth& a, onc_unix_params* uo) {
+                                              uint64_t slot, onc_auth& a, onc_unix_params* uo, uint32_t pad) {
     constexpr int32_t kShort = Rules<ONC_DECODE_SLICE>::kShort;
     uint32_t fl;
     ONC_RD(fl);
@@ -107,7 +123,7 @@ __device__ __forceinline__ int32_t auth_slice(const Rd& R, uint32_t& pos, uint32
             gids[g] = v;
         }
         if (pos - start != n) return ONC_ERR_INVALID_AUTH_DATA;          // unix_params.rs:117-119
-        put_unix(uo + slot, stamp, uid, gid, ng, rec_off + name_pos, nl, gids);
+        put_unix(uo + slot, stamp, uid, gid, ng, rec_off + name_pos, nl, gids, pad);
         a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
         a.ref = slot;
         return ONC_OK;
@@ -127,7 +143,7 @@ __device__ __forceinline__ int32_t auth_slice(const Rd& R, uint32_t& pos, uint32
 // first cut with try_array(200) (bytes_ext.rs:25-42); AUTH_UNIX is parsed
 // inside that slice (unix_params.rs:252-276) and must fill it exactly.
 __device__ __forceinline__ int32_t auth_bytes(const Rd& R, uint32_t& pos, uint32_t end, uint64_t rec_off,
-                                              uint64_t slot, onc_auth& a, onc_unix_params* uo) {
+                                              uint64_t slot, onc_auth& a, onc_unix_params* uo, uint32_t pad) {
     constexpr int32_t kShort = Rules<ONC_DECODE_BYTES>::kShort;
     uint32_t fl, n;
     ONC_RD(fl);
@@ -166,7 +182,7 @@ __device__ __forceinline__ int32_t auth_bytes(const Rd& R, uint32_t& pos, uint32
 #undef ONC_RDQ
         // params.serialised_len() != auth_data.len() -> InvalidAuthData (flavor.rs:204-208)
         if (20u + nl + pad4(nl) + 4u * ng != n) return ONC_ERR_INVALID_AUTH_DATA;
-        put_unix(uo + slot, stamp, uid, gid, ng, rec_off + name_pos, nl, gids);
+        put_unix(uo + slot, stamp, uid, gid, ng, rec_off + name_pos, nl, gids, pad);
         a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
         a.ref = slot;
         return ONC_OK;
@@ -179,9 +195,9 @@ __device__ __forceinline__ int32_t auth_bytes(const Rd& R, uint32_t& pos, uint32
 
 template <int MODE>
 __device__ __forceinline__ int32_t auth_any(const Rd& R, uint32_t& pos, uint32_t end, uint64_t rec_off,
-                                            uint64_t slot, onc_auth& a, onc_unix_params* uo) {
-    if (MODE == ONC_DECODE_BYTES) return auth_bytes(R, pos, end, rec_off, slot, a, uo);
-    return auth_slice(R, pos, end, rec_off, slot, a, uo);
+                                            uint64_t slot, onc_auth& a, onc_unix_params* uo, uint32_t pad) {
+    if (MODE == ONC_DECODE_BYTES) return auth_bytes(R, pos, end, rec_off, slot, a, uo, pad);
+    return auth_slice(R, pos, end, rec_off, slot, a, uo, pad);
 }
 
 // RpcMessage::try_from (rpc_message.rs:243-271 / :277-313), flattened.
@@ -216,9 +232,10 @@ __device__ __forceinline__ int32_t parse_record(const Rd& R, uint64_t L, uint64_
         ONC_RD(m.u.call.program);
         ONC_RD(m.u.call.program_version);
         ONC_RD(m.u.call.procedure);
-        int32_t st = auth_any<MODE>(R, pos, end, rec_off, 2 * i, m.cred, uo);
+        int32_t st = auth_any<MODE>(R, pos, end, rec_off, 2 * i, m.cred, uo, 1u);
         if (st != ONC_OK) return st;
-        st = auth_any<MODE>(R, pos, end, rec_off, 2 * i + 1, m.verf, uo);
+        const uint32_t vpad = (m.cred.kind_len >> 24) == ONC_KIND_UNIX ? 0u : 2u;
+        st = auth_any<MODE>(R, pos, end, rec_off, 2 * i + 1, m.verf, uo, vpad);
         if (st != ONC_OK) return st;
         m.payload_off = rec_off + pos;                     // call_body.rs:53-59 (zero copy)
         m.payload_len = end - pos;
@@ -232,7 +249,7 @@ __device__ __forceinline__ int32_t parse_record(const Rd& R, uint64_t L, uint64_
     ONC_RD(v);
     if (v == ONC_REPLY_ACCEPTED) {
         m.reply_stat = ONC_REPLY_ACCEPTED;
-        const int32_t st = auth_any<MODE>(R, pos, end, rec_off, 2 * i + 1, m.verf, uo);
+        const int32_t st = auth_any<MODE>(R, pos, end, rec_off, 2 * i + 1, m.verf, uo, 2u);
         if (st != ONC_OK) return st;
         ONC_RD(v);
         m.stat = uint8_t(v);

@@ -337,8 +337,8 @@ int main(int argc, char** argv) {
         {"img_u1_ntst", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<1, 2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
         {"img_u1_ntboth", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<1, 3>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
         {"img_u2_ntboth", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<2, 3>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u1_occ6", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<1, 0, 6>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
-        {"img_u2_nt_occ6", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<2, 3, 6>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u1_ntst_occ5", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<1, 2, 5>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
+        {"img_u2_ntst_occ5", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<2, 2, 5>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
         {"img_u2_ntst", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<2, 2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
         {"img_u4_ntboth", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<4, 3>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
         {"img_u2", true, [&] { hipLaunchKernelGGL((enc_emit_kernel_t<2>), dim3(uint32_t((tiles + 3) / 4)), dim3(256), 0, 0, a2); }},
