@@ -114,7 +114,12 @@ constexpr int kFastWaves = 4;                 // wave tiles per enc_emit workgro
 // at the 4-aligned address below the window + v_alignbyte, then a byte
 // rotation and a byte-masked merge (v_bfi).
 constexpr int kImgChunks = 248;               // image capacity per span (3968 B: 6 workgroups per CU)
-constexpr int kMap2Cap = 512;                 // granules per span (granule = 4 chunks, doubled to fit)
+#ifndef ONC_MAP_CAP
+#define ONC_MAP_CAP 512
+#define ONC_GSH_MIN 2
+#endif
+constexpr int kMap2Cap = ONC_MAP_CAP;         // granules per span (granule = 4 chunks, doubled to fit; an
+                                              // exact 2048-entry chunk map measured no faster)
 constexpr int kEmitChunkUnroll = 2;           // chunks per lane per step (2 + nontemporal stores: -5 % vs 1)
 constexpr int kEmitNT = 2;                    // nontemporal output stores (loads: measured slower)
 constexpr uint64_t kSpanBytesMax = 1ull << 30;  // a span's offsets fit uint32 (one record may exceed it)
@@ -200,7 +205,8 @@ __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, 
         for (int u = 0; u < kU; ++u) {
             const int32_t c = min(step + lane + 64 * u, NCe - 1);
             int r = T.map[c >> gsh];
-            while (c >= T.ent[r + 1].x) ++r;
+            if (gsh != 0)                                  // exact owner when a granule is one chunk
+                while (c >= T.ent[r + 1].x) ++r;
             const int4 m = T.ent[r];
             const uint4 q = T.pay[r];
             const int32_t s = c - m.w - (c >= m.z ? m.z - m.y : 0);
@@ -320,7 +326,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         const int64_t npx = active ? np : 0;
         const int64_t NP = int64_t(wave_incl_scan_u64(uint64_t(npx))) - npx;   // lanes < lo_rec add 0
         const int32_t NC = int32_t(((S1 + 15) >> 4) - C0);
-        uint32_t gsh = 2;                              // granule = 4 chunks, doubled until the span fits
+        uint32_t gsh = ONC_GSH_MIN;                    // granule = 4 chunks, doubled until the span fits
         while ((NC >> gsh) >= kMap2Cap) ++gsh;
         const uint64_t nonempty = __ballot(active && len != 0);
         if (active) {
