@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -20,6 +21,7 @@ struct onc_codec {
     uint64_t scratch_tiles = 0;
     uint8_t* frame_scratch = nullptr;   // onc_frame_stream per-chunk state
     uint64_t frame_chunks = 0;
+    bool force_scan = false;   // ONC_RPC_FORCE_SCAN=1 at create: always launch the block scan (tests)
     uint32_t timing = 0;   // bitmask of ONC_K_* ids whose launches are bracketed
     struct Pending {
         int kernel;
@@ -123,6 +125,8 @@ int onc_codec_create(onc_codec** out, int device, void* hip_stream) {
     onc_codec* c = new onc_codec();
     c->device = device;
     c->stream = static_cast<hipStream_t>(hip_stream);
+    const char* fs = getenv("ONC_RPC_FORCE_SCAN");
+    c->force_scan = fs && fs[0] == '1';
     if (set_device(c) != ONC_RC_OK) {
         delete c;
         return ONC_RC_EHIP;
@@ -303,13 +307,18 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
     bind_scratch(c, a);
     // enc_len: plans + tile/workgroup totals; scan: workgroup bases (and the
     // grand total into rec_off[n]); enc_emit: the bytes.
+    // Up to kFusedBlocks workgroups, enc_emit sums the workgroup totals
+    // itself and the scan launch is skipped.
+    const uint64_t nblk = onc::num_len_blocks(batch->n);
+    a.fused_base = nblk <= onc::kFusedBlocks && !c->force_scan;
     rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
-    const uint64_t nblk = onc::num_len_blocks(batch->n);
-    rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
-        return onc::launch_scan_tiles(a.block_sum, a.block_base, nblk, 0, rec_off + batch->n, c->stream);
-    });
-    if (rc != ONC_RC_OK) return rc;
+    if (!a.fused_base) {
+        rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
+            return onc::launch_scan_tiles(a.block_sum, a.block_base, nblk, 0, rec_off + batch->n, c->stream);
+        });
+        if (rc != ONC_RC_OK) return rc;
+    }
     return run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
 }
 

@@ -43,6 +43,28 @@ __device__ __forceinline__ T gload(uintptr_t a) {
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// A whole 64-byte descriptor as four dwordx4 loads. Callers issue these
+// with the other loads of their prologue and pin the registers
+// (pin_msg) before the first use, so all of them cost one memory round
+// trip: left alone, the compiler narrows the load to the fields each branch
+// of the planner reads and sinks each piece into its branch, one dependent
+// round trip per field.
+struct MsgRegs {
+    u32x4 q[4];
+};
+__device__ __forceinline__ MsgRegs issue_msg(const onc_msg* p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    MsgRegs r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r.q[k] = gload<u32x4>(a + 16 * k);
+    return r;
+}
+__device__ __forceinline__ onc_msg as_msg(const MsgRegs& r) {
+    onc_msg m;
+    __builtin_memcpy(&m, &r, sizeof(m));
+    return m;
+}
+
 // Four stream bytes at absolute byte address `addr`, bytes at or beyond
 // `lim` read as zero. Precondition: addr < lim. Only aligned dwords that
 // contain at least one byte < lim are touched, so the read never leaves

@@ -27,8 +27,11 @@ namespace onc {
 // (160 B: an AUTH_UNIX call with 16 gids and a 16-byte machine name). The
 // window is laid out [word][lane] so that lanes parsing the same field hit
 // distinct banks. Reads past what was loaded fall back to global loads.
-constexpr uint32_t kWin1 = 4;
-constexpr uint32_t kWinChunks = 10;
+#ifndef ONC_DEC_WIN
+#define ONC_DEC_WIN 10
+#endif
+constexpr uint32_t kWin1 = ONC_DEC_WIN < 4 ? ONC_DEC_WIN : 4;
+constexpr uint32_t kWinChunks = ONC_DEC_WIN;
 constexpr uint32_t kWinWords = 4 * kWinChunks;
 
 struct Rd {
@@ -371,7 +374,7 @@ __global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
         }
         const uint32_t want = min(avail, (q0 + need + 15) >> 4);
         if (want > nch) {
-            u32x4 w[kWinChunks - kWin1];
+            u32x4 w[kWinChunks > kWin1 ? kWinChunks - kWin1 : 1];
 #pragma unroll
             for (uint32_t j = kWin1; j < kWinChunks; ++j)
                 if (j < want) w[j - kWin1] = gload<u32x4>(win + 16 * j);

@@ -25,28 +25,44 @@ namespace onc {
 
 // Per-record plan + per-tile byte totals: tile = kEmitRecs (64) records =
 // one wavefront scan (lane 63 writes the total); a workgroup of kLenRecs =
-// 1024 lanes (16 waves, one record each) writes its total for the scan.
-__global__ __launch_bounds__(kLenRecs) void enc_len_kernel(EncArgs a) {
-    __shared__ uint64_t s_wave[kLenRecs / 64];
+// 1024 records writes its total for the scan. Each lane plans kLenPer (2)
+// records, one of each of its wave's two tiles (stores stay coalesced), with
+// both descriptors' loads issued before either is used: 512-thread
+// workgroups, half the waves of one record per lane, so the whole grid is
+// resident at once (1M records: 7.8k waves on 8k slots) instead of 1.9
+// rounds of workgroups.
+constexpr int kLenPer = 2;
+constexpr int kLenThreads = kLenRecs / kLenPer;
+__global__ __launch_bounds__(kLenThreads) void enc_len_kernel(EncArgs a) {
+    __shared__ uint64_t s_wave[kLenThreads / 64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t r = uint64_t(blockIdx.x) * kLenRecs + threadIdx.x;
-    uint64_t len = 0;
-    if (r < a.n) {
-        const onc_msg d = a.msgs[r];
-        const RecPlan p = plan_record(d, a.unix);
-        len = p.len;
-        a.status[r] = p.status;
-        if (a.rec_len) a.rec_len[r] = uint32_t(len);
+    const uint64_t rw = uint64_t(blockIdx.x) * kLenRecs + uint64_t(wv) * (64 * kLenPer);
+    onc_msg d[kLenPer];
+#pragma unroll
+    for (int k = 0; k < kLenPer; ++k) {
+        const uint64_t r = rw + 64 * k + lane;
+        if (r < a.n) d[k] = a.msgs[r];
     }
-    const uint64_t incl = wave_incl_scan_u64(len);
-    const uint64_t tile = r / kEmitRecs;
-    if (lane == 63) {
-        if (tile * kEmitRecs < a.n) a.tile_sum[tile] = incl;
-        s_wave[wv] = incl;
+    uint64_t wsum = 0;
+#pragma unroll
+    for (int k = 0; k < kLenPer; ++k) {
+        const uint64_t r = rw + 64 * k + lane;
+        uint64_t len = 0;
+        if (r < a.n) {
+            const RecPlan p = plan_record(d[k], a.unix);
+            len = p.len;
+            a.status[r] = p.status;
+            if (a.rec_len) a.rec_len[r] = uint32_t(len);
+        }
+        const uint64_t incl = wave_incl_scan_u64(len);
+        const uint64_t tile = (rw + 64 * k) / kEmitRecs;
+        if (lane == 63 && tile * kEmitRecs < a.n) a.tile_sum[tile] = incl;
+        wsum += __shfl(incl, 63, 64);
     }
+    if (lane == 0) s_wave[wv] = wsum;
     __syncthreads();
     if (threadIdx.x < 64) {
-        const uint64_t v = threadIdx.x < kLenRecs / 64 ? s_wave[threadIdx.x] : 0;
+        const uint64_t v = threadIdx.x < kLenThreads / 64 ? s_wave[threadIdx.x] : 0;
         const uint64_t t = wave_incl_scan_u64(v);
         if (threadIdx.x == 63) a.block_sum[blockIdx.x] = t;
     }
@@ -74,15 +90,48 @@ __device__ __forceinline__ void store_chunk(uint8_t* out, uint64_t o, uint64_t l
 }
 
 // Byte offset of tile `tile` in the output: base of its enc_len workgroup
-// (scan of the workgroup totals) + totals of the tiles before it there
-// (lane i loads tile i of the workgroup; one wave reduction). Wave-uniform.
-__device__ __forceinline__ uint64_t tile_start(const EncArgs& a, uint64_t tile) {
+// + totals of the tiles before it there (lane i loads tile i of the
+// workgroup; one wave reduction). The base is the scan kernel's output, or
+// (kFused) the sum of the workgroup totals before it, lane l adding
+// workgroups l, l + 64, ... Split in two so that the caller can issue its
+// own loads between: tile_loads issues every load (no branches, clamped
+// indices), tile_reduce consumes them. Wave-uniform result.
+template <bool kFused>
+struct TileLoads {
+    static constexpr int kW = kFused ? int(kFusedBlocks / 64) : 1;
+    uint64_t v;
+    uint64_t w[kW];
+};
+
+template <bool kFused>
+__device__ __forceinline__ TileLoads<kFused> tile_loads(const EncArgs& a, uint64_t tile) {
     const int lane = threadIdx.x & 63;
     const uint64_t blk = tile / (kLenRecs / kEmitRecs);
     const uint64_t t0 = blk * (kLenRecs / kEmitRecs);
-    const uint64_t v = t0 + lane < tile ? a.tile_sum[t0 + lane] : 0;
-    const uint64_t base = a.block_base[blk];
-    return base + __shfl(wave_incl_scan_u64(v), 63, 64);
+    TileLoads<kFused> t;
+    t.v = a.tile_sum[t0 + (lane < kLenRecs / kEmitRecs ? lane : 0)];
+    if (kFused) {
+        const uint64_t nb = num_len_blocks(a.n);
+#pragma unroll
+        for (int k = 0; k < TileLoads<kFused>::kW; ++k) t.w[k] = a.block_sum[min(uint64_t(lane) + uint64_t(64 * k), nb - 1)];
+    } else {
+        t.w[0] = a.block_base[blk];
+    }
+    return t;
+}
+
+template <bool kFused>
+__device__ __forceinline__ uint64_t tile_reduce(const TileLoads<kFused>& t, uint64_t tile) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t blk = tile / (kLenRecs / kEmitRecs);
+    const uint64_t t0 = blk * (kLenRecs / kEmitRecs);
+    uint64_t v = t0 + lane < tile ? t.v : 0;
+    if (kFused) {
+#pragma unroll
+        for (int k = 0; k < TileLoads<kFused>::kW; ++k) v += lane + 64ull * k < blk ? t.w[k] : 0;
+        return __shfl(wave_incl_scan_u64(v), 63, 64);
+    }
+    return t.w[0] + __shfl(wave_incl_scan_u64(v), 63, 64);
 }
 
 constexpr int kFastWaves = 4;                 // wave tiles per enc_emit workgroup
@@ -120,7 +169,10 @@ constexpr int kImgChunks = 248;               // image capacity per span (3968 B
 #endif
 constexpr int kMap2Cap = ONC_MAP_CAP;         // granules per span (granule = 4 chunks, doubled to fit; an
                                               // exact 2048-entry chunk map measured no faster)
-constexpr int kEmitChunkUnroll = 2;           // chunks per lane per step (2 + nontemporal stores: -5 % vs 1)
+#ifndef ONC_EMIT_U
+#define ONC_EMIT_U 1
+#endif
+constexpr int kEmitChunkUnroll = ONC_EMIT_U;    // chunks per lane per pipelined step
 constexpr int kEmitNT = 2;                    // nontemporal output stores (loads: measured slower)
 constexpr uint64_t kSpanBytesMax = 1ull << 30;  // a span's offsets fit uint32 (one record may exceed it)
 // a record's own non-pure chunks: header <= 4 * (7 + 2 * 52) bytes, + the
@@ -192,76 +244,134 @@ __device__ __forceinline__ void merge_bytes(const uint32_t X[4], const uint4& L,
     }
 }
 
+// Per-chunk plan of the stream loop: payload load address (or a dummy),
+// image slot, and the merge selector (word path: bits 0-3 dword i is
+// payload, bits 4-5 rotation; byte path: r | lo << 8 | hi << 16).
+struct ChunkPlan {
+    uintptr_t A;
+    int32_t slot;
+    uint32_t sel;
+};
+
+template <bool kByte>
+__device__ __forceinline__ ChunkPlan plan_chunk(const ImgTile& T, uint32_t gsh, uint64_t B0, int32_t c,
+                                                uintptr_t dummy) {
+    int r = T.map[c >> gsh];
+    if (gsh != 0)                                  // exact owner when a granule is one chunk
+        while (c >= T.ent[r + 1].x) ++r;
+    const int4 m = T.ent[r];
+    const uint4 q = T.pay[r];
+    const int32_t s = c - m.w - (c >= m.z ? m.z - m.y : 0);
+    ChunkPlan P;
+    P.slot = s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s);
+    const uint32_t o = uint32_t(c) << 4;
+    const bool hasp = q.x < q.y && o < q.y && o + 16 > q.x;
+    const uint32_t x = max(q.x, min(o, q.y - 16));            // clamped window start
+    const uint64_t sbase = uint64_t(q.z) | (uint64_t(q.w) << 32);
+    P.A = hasp ? sbase + B0 + x : dummy;
+    if (kByte) {
+        const uint32_t lo = hasp ? (q.x > o ? q.x - o : 0u) : 0u;
+        const uint32_t hi = hasp ? min(q.y - o, 16u) : 0u;
+        P.sel = ((o - x) & 15u) | (lo << 8) | (hi << 16);
+    } else {
+        uint32_t pm = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pm |= (o + 4 * i >= q.x && o + 4 * i < q.y) ? (1u << i) : 0u;
+        P.sel = (hasp ? pm : 0u) | (((o - x) >> 2) & 3u) << 4;
+    }
+    return P;
+}
+
+template <int kNT, bool kByte>
+__device__ __forceinline__ void load_chunk(const ChunkPlan& P, uint32_t X[4]) {
+    if (kByte) {
+        load16_unaligned(P.A, X);
+    } else {
+        u32x4_a4 w;
+        if (kNT & 1) w = __builtin_nontemporal_load(reinterpret_cast<const ONC_GLOBAL u32x4_a4*>(P.A));
+        else w = gload<u32x4_a4>(P.A);
+        X[0] = w.x; X[1] = w.y; X[2] = w.z; X[3] = w.w;
+    }
+}
+
+template <bool kByte>
+__device__ __forceinline__ void merge_chunk(const ChunkPlan& P, const uint32_t X[4], const uint4& L, uint32_t v[4]) {
+    if (kByte) {
+        merge_bytes(X, L, P.sel & 15u, (P.sel >> 8) & 0xFFu, P.sel >> 16, v);
+    } else {
+        const u32x4_a4 w = {X[0], X[1], X[2], X[3]};
+        merge_words(w, L, P.sel, v);
+    }
+}
+
+// The stream loop over the span's full chunks, software-pipelined with two
+// register sets: step s + 1's payload loads and image reads are issued
+// before step s is merged and stored. gfx950 counts loads and stores on one
+// in-order vmcnt, so a load issued after a store cannot be waited for
+// without waiting for the store too; issued before it, waiting for the
+// loads leaves the previous step's stores in flight. The loop therefore has
+// no data-dependent VMEM control flow: every step issues exactly kU loads
+// and kU stores (lanes past the last full chunk repeat it — same bytes to
+// the same address), and the next step is always issued (the surplus
+// after the last step re-reads the last chunk). The one or two partial
+// chunks at the span's edges are written after the loop, with byte stores
+// of only the span's bytes.
 template <int kU, int kNT, bool kByte>
 __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, uint32_t gsh, uint64_t B0,
                                             uint64_t S0, uint64_t E, int32_t NCe, uintptr_t dummy) {
     const int lane = threadIdx.x & 63;
-    for (int32_t step = 0; step < NCe; step += 64 * kU) {
-        uintptr_t A[kU];
-        int32_t slot[kU];
-        uint32_t sel[kU];      // word path: bits 0-3 dword i is payload, bits 4-5 rotation;
-                               // byte path: r | lo << 8 | hi << 16
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const int32_t c = min(step + lane + 64 * u, NCe - 1);
-            int r = T.map[c >> gsh];
-            if (gsh != 0)                                  // exact owner when a granule is one chunk
-                while (c >= T.ent[r + 1].x) ++r;
-            const int4 m = T.ent[r];
-            const uint4 q = T.pay[r];
-            const int32_t s = c - m.w - (c >= m.z ? m.z - m.y : 0);
-            slot[u] = s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s);
-            const uint32_t o = uint32_t(c) << 4;
-            const bool hasp = q.x < q.y && o < q.y && o + 16 > q.x;
-            const uint32_t x = max(q.x, min(o, q.y - 16));            // clamped window start
-            const uint64_t sbase = uint64_t(q.z) | (uint64_t(q.w) << 32);
-            A[u] = hasp ? sbase + B0 + x : dummy;
-            if (kByte) {
-                const uint32_t lo = hasp ? (q.x > o ? q.x - o : 0u) : 0u;
-                const uint32_t hi = hasp ? min(q.y - o, 16u) : 0u;
-                sel[u] = ((o - x) & 15u) | (lo << 8) | (hi << 16);
-            } else {
-                uint32_t pm = 0;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) pm |= (o + 4 * i >= q.x && o + 4 * i < q.y) ? (1u << i) : 0u;
-                sel[u] = (hasp ? pm : 0u) | (((o - x) >> 2) & 3u) << 4;
-            }
+    constexpr int32_t S = 64 * kU;
+    const int32_t cf = S0 > B0 ? 1 : 0;                 // chunk 0 partial: span starts inside it
+    const int32_t cl = (E & 15) ? NCe - 1 : NCe;          // full chunks [cf, cl)
+    if (cl > cf) {
+        ChunkPlan Pa[kU], Pb[kU];
+        uint32_t Xa[kU][4], Xb[kU][4];
+        uint4 La[kU], Lb[kU];
+#define ONC_ISSUE(P, X, L, base)                                                          \
+    _Pragma("unroll") for (int u = 0; u < kU; ++u) {                                     \
+        P[u] = plan_chunk<kByte>(T, gsh, B0, min((base) + lane + 64 * u, cl - 1), dummy);   \
+        load_chunk<kNT, kByte>(P[u], X[u]);                                               \
+        L[u] = T.img[P[u].slot];                                                          \
+    }
+#define ONC_CONSUME(P, X, L, base)                                                        \
+    _Pragma("unroll") for (int u = 0; u < kU; ++u) {                                     \
+        const int32_t c = min((base) + lane + 64 * u, cl - 1);                            \
+        uint32_t v[4];                                                                    \
+        merge_chunk<kByte>(P[u], X[u], L[u], v);                                          \
+        u32x4* d = reinterpret_cast<u32x4*>(a.out + B0 + (uint64_t(c) << 4));             \
+        if (kNT & 2) __builtin_nontemporal_store(u32x4{v[0], v[1], v[2], v[3]}, d);       \
+        else *d = u32x4{v[0], v[1], v[2], v[3]};                                          \
+    }
+        ONC_ISSUE(Pa, Xa, La, cf);
+        for (int32_t st = cf;; st += 2 * S) {
+            ONC_ISSUE(Pb, Xb, Lb, st + S);
+            ONC_CONSUME(Pa, Xa, La, st);
+            if (st + S >= cl) break;
+            ONC_ISSUE(Pa, Xa, La, st + 2 * S);
+            ONC_CONSUME(Pb, Xb, Lb, st + S);
+            if (st + 2 * S >= cl) break;
         }
-        uint32_t X[kU][4];
-        uint4 L[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            if (kByte) {
-                load16_unaligned(A[u], X[u]);
-            } else {
-                u32x4_a4 w;
-                if (kNT & 1) w = __builtin_nontemporal_load(reinterpret_cast<const ONC_GLOBAL u32x4_a4*>(A[u]));
-                else w = gload<u32x4_a4>(A[u]);
-                X[u][0] = w.x; X[u][1] = w.y; X[u][2] = w.z; X[u][3] = w.w;
-            }
-            L[u] = T.img[slot[u]];
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const int32_t c = step + lane + 64 * u;
-            if (c >= NCe) break;
-            uint32_t v[4];
-            if (kByte) {
-                merge_bytes(X[u], L[u], sel[u] & 15u, (sel[u] >> 8) & 0xFFu, sel[u] >> 16, v);
-            } else {
-                const u32x4_a4 w = {X[u][0], X[u][1], X[u][2], X[u][3]};
-                merge_words(w, L[u], sel[u], v);
-            }
-            const uint64_t o = B0 + (uint64_t(c) << 4);
-            if ((kNT & 2) && o >= S0 && o + 16 <= E)
-                __builtin_nontemporal_store(u32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<u32x4*>(a.out + o));
-            else
-                store_chunk(a.out, o, max(o, S0), min(o + 16, E), v);
-        }
+#undef ONC_ISSUE
+#undef ONC_CONSUME
+    }
+    // partial edge chunks: lane 0 the first (if the span starts inside it),
+    // lane 1 the last (if the span ends inside it and it is another chunk)
+    const bool e0 = lane == 0 && cf == 1;
+    const bool e1 = lane == 1 && cl == NCe - 1 && (NCe - 1 > 0 || cf == 0);
+    if (e0 || e1) {
+        const int32_t c = e0 ? 0 : NCe - 1;
+        const ChunkPlan P = plan_chunk<kByte>(T, gsh, B0, c, dummy);
+        uint32_t X[4];
+        load_chunk<kNT, kByte>(P, X);
+        const uint4 L = T.img[P.slot];
+        uint32_t v[4];
+        merge_chunk<kByte>(P, X, L, v);
+        const uint64_t o = B0 + (uint64_t(c) << 4);
+        store_chunk(a.out, o, max(o, S0), min(o + 16, E), v);
     }
 }
 
-template <int kU, int kNT>
+template <int kU, int kNT, bool kFused>
 __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = tile * kEmitRecs;
@@ -269,12 +379,26 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
     const uintptr_t payload = reinterpret_cast<uintptr_t>(a.payload_arena);
 
-    const uint64_t T0 = tile_start(a, tile);
+    // Prologue: the tile-placement loads and this lane's descriptor issued
+    // together, one memory round trip before the planning starts.
+    TileLoads<kFused> tl = tile_loads<kFused>(a, tile);
+    MsgRegs mr = issue_msg(a.msgs + r0 + min(lane, nrec - 1));
+    if constexpr (kFused) {
+        static_assert(TileLoads<kFused>::kW == 16, "pin list below");
+        asm volatile("" : "+v"(mr.q[0]), "+v"(mr.q[1]), "+v"(mr.q[2]), "+v"(mr.q[3]), "+v"(tl.v),
+                     "+v"(tl.w[0]), "+v"(tl.w[1]), "+v"(tl.w[2]), "+v"(tl.w[3]), "+v"(tl.w[4]), "+v"(tl.w[5]),
+                     "+v"(tl.w[6]), "+v"(tl.w[7]), "+v"(tl.w[8]), "+v"(tl.w[9]), "+v"(tl.w[10]), "+v"(tl.w[11]),
+                     "+v"(tl.w[12]), "+v"(tl.w[13]), "+v"(tl.w[14]), "+v"(tl.w[15]));
+    } else {
+        asm volatile("" : "+v"(mr.q[0]), "+v"(mr.q[1]), "+v"(mr.q[2]), "+v"(mr.q[3]), "+v"(tl.v), "+v"(tl.w[0]));
+    }
+    const onc_msg dm = as_msg(mr);
+    const uint64_t T0 = tile_reduce<kFused>(tl, tile);
     uint64_t len = 0, poff = 0;
     uint32_t hw = 0;
     bool word_aligned = true;
     if (lane < nrec) {
-        const onc_msg d = a.msgs[r0 + lane];
+        const onc_msg& d = dm;
         const RecPlan p = plan_record(d, a.unix);   // the same function as enc_len: lengths agree
         len = p.len;
         hw = len ? meta_hw(p.meta) : 0;
@@ -287,6 +411,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     const uint64_t pst = start + 4ull * hw;
     if (lane < nrec) {
         a.rec_off[r0 + lane] = start;
+        if (r0 + lane + 1 == a.n) a.rec_off[a.n] = en;      // the grand total
         if (len != 0 && en > a.out_cap) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
     }
     const bool byte_mode = !(__all(word_aligned) && (T0 & 3) == 0);
@@ -339,7 +464,10 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                 // the record's non-pure bytes are contiguous in the image from
                 // image byte start - 16 (C0 + NP)
                 const uint64_t ibb = start - 16ull * uint64_t(C0 + NP);
-                const onc_msg d = a.msgs[r0 + lane];
+                // reloaded (an L2 hit) rather than kept live across the span loop
+                MsgRegs mr2 = issue_msg(a.msgs + r0 + lane);
+                asm volatile("" : "+v"(mr2.q[0]), "+v"(mr2.q[1]), "+v"(mr2.q[2]), "+v"(mr2.q[3]));
+                const onc_msg d = as_msg(mr2);
                 const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
                 ImgSink w{img32, uint32_t(ibb >> 2), 32u - 8u * uint32_t(ibb & 3), 0u};
                 put_header_words(d, uint32_t(len), src, w);
@@ -372,21 +500,26 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
 
 // kNT: bit 0 = nontemporal payload loads, bit 1 = nontemporal stores;
 // kOcc: workgroups per CU the register allocation must allow (0 = free)
-template <int kU, int kNT = 0, int kOcc = 0>
+template <int kU, int kNT = 0, int kOcc = 0, bool kFused = false>
 __global__ __launch_bounds__(64 * kFastWaves, kOcc ? kOcc * kFastWaves / 4 : 1) void enc_emit_kernel_t(EncArgs a) {
     __shared__ ImgTile s_tiles[kFastWaves];
     const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
-    if (tile < num_emit_tiles(a.n)) enc_emit_tile<kU, kNT>(a, s_tiles[threadIdx.x >> 6], tile);
+    if (tile < num_emit_tiles(a.n)) enc_emit_tile<kU, kNT, kFused>(a, s_tiles[threadIdx.x >> 6], tile);
 }
 
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(enc_len_kernel, dim3(uint32_t(num_len_blocks(a.n))), dim3(kLenRecs), 0, s, a);
+    hipLaunchKernelGGL(enc_len_kernel, dim3(uint32_t(num_len_blocks(a.n))), dim3(kLenThreads), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
     const uint64_t blocks = (num_emit_tiles(a.n) + kFastWaves - 1) / kFastWaves;
-    hipLaunchKernelGGL((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT>), dim3(uint32_t(blocks)), dim3(64 * kFastWaves), 0, s, a);
+    if (a.fused_base)
+        hipLaunchKernelGGL((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, true>), dim3(uint32_t(blocks)),
+                           dim3(64 * kFastWaves), 0, s, a);
+    else
+        hipLaunchKernelGGL((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, false>), dim3(uint32_t(blocks)),
+                           dim3(64 * kFastWaves), 0, s, a);
     return hipGetLastError();
 }
 

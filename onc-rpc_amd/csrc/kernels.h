@@ -23,8 +23,14 @@ struct EncArgs {
     uint32_t* rec_len;      // n, optional
     uint64_t* tile_sum;     // tiles
     uint64_t* block_sum;    // enc_len workgroups (kLenRecs records): byte totals
-    uint64_t* block_base;   // exclusive scan of block_sum
+    uint64_t* block_base;   // exclusive scan of block_sum (unused when fused_base)
+    uint32_t fused_base;    // enc_emit sums block_sum itself (<= kFusedBlocks workgroups; no scan launch)
 };
+
+// Batches of at most this many enc_len workgroups (1M records) skip the
+// scan launch: every enc_emit wave sums the block totals before its own
+// (16 coalesced u64 loads per lane, issued with its tile-total load).
+constexpr uint64_t kFusedBlocks = 1024;
 
 struct IovArgs {
     uint64_t n;

@@ -15,7 +15,7 @@ import numpy as np
 from . import layout as L
 
 _LIB = None
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libonc_rpc_amd.so")
+LIB_PATH = os.environ.get("ONC_RPC_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libonc_rpc_amd.so")
 
 K_NAMES = ["enc_len_kernel", "scan_tiles_kernel", "enc_emit_kernel", "decode_kernel",
            "len_tiles_kernel", "len_apply_kernel", "enc_fixup_kernel", "iov_len_kernel", "iov_emit_kernel",

@@ -1,0 +1,13 @@
+"""Print value + per-kernel averages of bench JSON lines (dev helper)."""
+import json
+import sys
+
+for f in sys.argv[1:]:
+    try:
+        d = json.loads(open(f).read().strip().splitlines()[-1])
+    except Exception as e:  # noqa: BLE001
+        print(f, "unreadable", e)
+        continue
+    k = d["kernels_breakdown_pass"]
+    print(f, round(d["value"], 1), round(d["ms_per_step"] * 1e3, 1), "us/step",
+          {n: round(v["avg_us"], 1) for n, v in k.items()}, "frac", round(d["roofline"]["frac"], 3))

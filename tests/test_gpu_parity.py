@@ -345,6 +345,28 @@ def test_full_size_config1_loopback(codec, R, oracle):
     assert out[lo * 300:hi * 300].cpu().numpy().tobytes() == o_wire
 
 
+def test_block_base_scan_path(R, oracle, monkeypatch):
+    """Encode places tiles either from enc_emit's own sum of the enc_len
+    workgroup totals (<= 1024 workgroups) or from the scan kernel: the
+    forced-scan codec and a batch above the fused limit (1.1M records) are
+    bit-exact vs the oracle as well."""
+    hb = S.mixed(6000, seed=21, pmin=0, pmax=700, exotic=0.2)
+    monkeypatch.setenv("ONC_RPC_FORCE_SCAN", "1")
+    c_scan = R.Codec(0)
+    monkeypatch.delenv("ONC_RPC_FORCE_SCAN")
+    try:
+        gpu_vs_oracle_encode(R, c_scan, oracle, hb)
+    finally:
+        c_scan.close()
+    c = R.Codec(0)
+    try:
+        gpu_vs_oracle_encode(R, c, oracle, hb)
+        big = S.call_none(1_100_000, 13, seed=5)       # 1075 workgroups: scan launch, byte path
+        gpu_vs_oracle_encode(R, c, oracle, big)
+    finally:
+        c.close()
+
+
 # ---------------------------------------------------------------------------
 # Vectored encode (SURVEY §8(f) rank 2): headers + in-place payload slices.
 def iov_wire(hb, hdr, iov, st):

@@ -1,0 +1,156 @@
+// dec_lab.hip — A/B timing harness for decode ceilings (dev tool).
+//
+// Builds a configs[1] wire (1M x 300 B Call/AuthNone records) on the host,
+// times the product decode kernel and memory-only ceilings of the same
+// access pattern, interleaved in one process.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/dec_lab.hip -o tools/dec_lab
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <vector>
+
+#include "../onc-rpc_amd/csrc/decode.hip"
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+using namespace onc;
+
+// read-only: the 64-byte window of every record, folded into one status word
+template <int NCH>
+__global__ __launch_bounds__(256) void l_read(DecArgs a) {
+    const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const uint64_t b = a.rec_off[i];
+    const uintptr_t win = (reinterpret_cast<uintptr_t>(a.wire) + b) & ~uintptr_t(15);
+    u32x4 v[NCH];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) v[j] = gload<u32x4>(win + 16 * j);
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) x ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+    a.out.status[i] = int32_t(x == 0x12345678u);
+}
+
+// read window + write descriptors (LDS staged) + status/aux
+template <int NCH>
+__global__ __launch_bounds__(256) void l_rw(DecArgs a) {
+    __shared__ uint4 st[256 * 4];
+    const int t = threadIdx.x;
+    const uint64_t i0 = uint64_t(blockIdx.x) * 256, i = i0 + t;
+    uint4 m[4] = {};
+    if (i < a.n) {
+        const uint64_t b = a.rec_off[i];
+        const uintptr_t win = (reinterpret_cast<uintptr_t>(a.wire) + b) & ~uintptr_t(15);
+        u32x4 v[NCH];
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) v[j] = gload<u32x4>(win + 16 * j);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m[j] = make_uint4(v[j % NCH].x, v[j % NCH].y, uint32_t(b), v[j % NCH].w);
+        a.out.status[i] = 0;
+        a.out.aux0[i] = 0;
+        a.out.aux1[i] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st[4 * t + k] = m[k];
+    __syncthreads();
+    const uint64_t nblk = min(uint64_t(256), a.n - i0);
+    uint4* dst = reinterpret_cast<uint4*>(a.out.msgs + i0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t j = uint32_t(k * 256 + t);
+        if (j < 4 * nblk) dst[j] = st[j];
+    }
+}
+
+// write-only: descriptors + status/aux
+__global__ __launch_bounds__(256) void l_write(DecArgs a) {
+    const uint64_t i0 = uint64_t(blockIdx.x) * 256, i = i0 + threadIdx.x;
+    if (i < a.n) {
+        a.out.status[i] = 0;
+        a.out.aux0[i] = 0;
+        a.out.aux1[i] = 0;
+    }
+    const uint64_t nblk = min(uint64_t(256), a.n - i0);
+    uint4* dst = reinterpret_cast<uint4*>(a.out.msgs + i0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t j = uint32_t(k * 256 + threadIdx.x);
+        if (j < 4 * nblk) dst[j] = make_uint4(j, 0, 0, 0);
+    }
+}
+
+static void put32(uint8_t* p, uint32_t v) {
+    p[0] = v >> 24; p[1] = v >> 16; p[2] = v >> 8; p[3] = v;
+}
+
+int main(int argc, char** argv) {
+    const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 1000000;
+    const uint32_t W = 300;
+    std::vector<uint8_t> wire(n * W + 64);
+    std::vector<uint64_t> off(n + 1);
+    for (uint64_t i = 0; i < n; ++i) {
+        uint8_t* p = &wire[i * W];
+        off[i] = i * W;
+        put32(p, 0x80000000u | (W - 4));
+        put32(p + 4, uint32_t(i));
+        put32(p + 8, 0); put32(p + 12, 2); put32(p + 16, 100003); put32(p + 20, 4); put32(p + 24, 1);
+        put32(p + 28, 0); put32(p + 32, 0); put32(p + 36, 0); put32(p + 40, 0);
+        for (uint32_t k = 44; k < W; ++k) p[k] = uint8_t(i * 7 + k);
+    }
+    off[n] = n * W;
+    uint8_t* dw; uint64_t* doff; onc_msg* dm; onc_unix_params* du; int32_t* ds; uint32_t *da0, *da1;
+    CK(hipMalloc(&dw, wire.size()));
+    CK(hipMalloc(&doff, 8 * (n + 1)));
+    CK(hipMalloc(&dm, sizeof(onc_msg) * n));
+    CK(hipMalloc(&du, sizeof(onc_unix_params) * 2 * n));
+    CK(hipMalloc(&ds, 4 * n)); CK(hipMalloc(&da0, 4 * n)); CK(hipMalloc(&da1, 4 * n));
+    CK(hipMemcpy(dw, wire.data(), wire.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(doff, off.data(), 8 * (n + 1), hipMemcpyHostToDevice));
+    // 512 MiB scrub buffer between reps so nothing is served from MALL
+    void* scrub; const size_t scrub_b = size_t(512) << 20;
+    CK(hipMalloc(&scrub, scrub_b));
+    DecArgs a{};
+    a.wire = dw; a.rec_off = doff; a.n = n;
+    a.out.msgs = dm; a.out.unix_params = du; a.out.status = ds; a.out.aux0 = da0; a.out.aux1 = da1;
+    const uint32_t grid = uint32_t((n + 255) / 256);
+    struct V { const char* name; std::function<void()> run; std::vector<float> t; };
+    std::vector<V> vs = {
+        {"product decode<slice>", [&] { hipLaunchKernelGGL(decode_kernel<ONC_DECODE_SLICE>, dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"read 4 chunks", [&] { hipLaunchKernelGGL(l_read<4>, dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"read 3 chunks", [&] { hipLaunchKernelGGL(l_read<3>, dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"read 4 + write", [&] { hipLaunchKernelGGL(l_rw<4>, dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"read 3 + write", [&] { hipLaunchKernelGGL(l_rw<3>, dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"write only", [&] { hipLaunchKernelGGL(l_write, dim3(grid), dim3(256), 0, 0, a); }, {}},
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    const bool cold = getenv("LAB_WARM") == nullptr;
+    for (int rep = 0; rep < 25; ++rep) {
+        for (auto& v : vs) {
+            if (cold) CK(hipMemsetAsync(scrub, rep, scrub_b, 0));
+            CK(hipEventRecord(e0, 0));
+            v.run();
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+            if (rep >= 5) v.t.push_back(ms * 1000.f);
+        }
+    }
+    printf("n=%llu cold=%d\n", (unsigned long long)n, int(cold));
+    for (auto& v : vs) {
+        std::sort(v.t.begin(), v.t.end());
+        printf("%-26s median %7.1f us  min %7.1f\n", v.name, v.t[v.t.size() / 2], v.t[0]);
+    }
+    return 0;
+}
