@@ -515,6 +515,9 @@ def main():
         "iov_emit_kernel": 0,
         "frame_chunks_kernel": 0,
         "frame_write_kernel": 8 * n,
+        "frame_verify_kernel": 0,
+        "frame_walk_kernel": 0,
+        "frame_counts_kernel": 0,
     }
     kern = {}
     for name, (tot_ms, cnt) in breakdown.items():

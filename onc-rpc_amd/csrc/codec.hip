@@ -21,6 +21,7 @@ struct onc_codec {
     uint64_t scratch_tiles = 0;
     uint8_t* frame_scratch = nullptr;   // onc_frame_stream per-chunk state
     uint64_t frame_chunks = 0;
+    uint64_t frame_chunk = onc::kFrameChunkDefault;   // ONC_RPC_FRAME_CHUNK at create (bytes, >= 64)
     bool force_scan = false;   // ONC_RPC_FORCE_SCAN=1 at create: always launch the block scan (tests)
     uint32_t timing = 0;   // bitmask of ONC_K_* ids whose launches are bracketed
     struct Pending {
@@ -127,6 +128,11 @@ int onc_codec_create(onc_codec** out, int device, void* hip_stream) {
     c->stream = static_cast<hipStream_t>(hip_stream);
     const char* fs = getenv("ONC_RPC_FORCE_SCAN");
     c->force_scan = fs && fs[0] == '1';
+    const char* fc = getenv("ONC_RPC_FRAME_CHUNK");
+    if (fc) {
+        const unsigned long long v = strtoull(fc, nullptr, 10);
+        if (v >= 64) c->frame_chunk = v;
+    }
     if (set_device(c) != ONC_RC_OK) {
         delete c;
         return ONC_RC_EHIP;
@@ -211,6 +217,9 @@ const char* onc_kernel_name(int k) {
         case ONC_K_IOV_EMIT: return "iov_emit_kernel";
         case ONC_K_FRAME: return "frame_chunks_kernel";
         case ONC_K_FRAME_WRITE: return "frame_write_kernel";
+        case ONC_K_FRAME_VERIFY: return "frame_verify_kernel";
+        case ONC_K_FRAME_WALK: return "frame_walk_kernel";
+        case ONC_K_FRAME_COUNTS: return "frame_counts_kernel";
         default: return "?";
     }
 }
@@ -380,7 +389,8 @@ int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* 
     if (e == hipSuccess) e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
     if (e != hipSuccess) return fail(c, e, "hipMemsetAsync");
     if (len == 0 || max_records == 0) return ONC_RC_OK;   // nothing framed, nothing consumed
-    const uint64_t P = (len + onc::kFrameChunk - 1) / onc::kFrameChunk;
+    const uint64_t chunk = c->frame_chunk;
+    const uint64_t P = (len + chunk - 1) / chunk;
     if (P > c->frame_chunks) {
         uint64_t want = c->frame_chunks ? c->frame_chunks : 4096;
         while (want < P) want *= 2;
@@ -399,6 +409,7 @@ int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* 
     onc::FrameArgs a{};
     a.wire = wire;
     a.len = len;
+    a.chunk = chunk;
     a.nchunks = P;
     a.max_records = max_records;
     a.rec_off = rec_off;
@@ -424,6 +435,12 @@ int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* 
     a.first_fail = tail + 2 * (nt + 1);
     a.first_stop = a.first_fail + 1;
     int rc = run(c, ONC_K_FRAME, "frame_chunks", [&] { return onc::launch_frame_chunks(a, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    rc = run(c, ONC_K_FRAME_VERIFY, "frame_verify", [&] { return onc::launch_frame_verify(a, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    rc = run(c, ONC_K_FRAME_WALK, "frame_walk", [&] { return onc::launch_frame_walk(a, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    rc = run(c, ONC_K_FRAME_COUNTS, "frame_counts", [&] { return onc::launch_frame_counts(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
     rc = run(c, ONC_K_LEN_TILES, "len_tiles", [&] { return onc::launch_len_tiles(a.cnt_eff, P, tile_sum, c->stream); });
     if (rc != ONC_RC_OK) return rc;

@@ -7,14 +7,16 @@
 // record k's header: a serial chain. Here it is framed in parallel by
 // speculation + verification, with the same result as the serial loop:
 //
-//   frame_chunks  lane per 4 KiB chunk: guess the first record start in the
-//                 chunk (the first position that looks like an ONC-RPC
-//                 header: last-fragment bit, length within the buffer,
-//                 message type 0 with rpcvers 2 or 1 with reply_stat 0/1),
-//                 then follow the exact chain (header length only, as the
-//                 reference does) out of the chunk: exit position and record
-//                 count, or where and why the chain stops. Chunk 0 starts
-//                 at byte 0.
+//   frame_guess   wave per chunk (64 KiB by default; ONC_RPC_FRAME_CHUNK):
+//                 guess the first record start in the chunk (the first
+//                 position that looks like an ONC-RPC header: last-fragment
+//                 bit, length within the buffer, message type 0 with
+//                 rpcvers 2 or 1 with reply_stat 0/1) with a coalesced
+//                 1 KiB-per-step sweep. Chunk 0 starts at byte 0.
+//   frame_chunks  lane per chunk: follow the exact chain from the guess
+//                 (header length only, as the reference does) out of the
+//                 chunk: exit position and record count, or where and why
+//                 the chain stops.
 //   frame_verify  lane per chunk: a guessed chunk is consistent when its
 //                 chain lands exactly on the guess of the chunk it lands in
 //                 and every chunk it jumps over has no guess. Because chunk 0
@@ -94,69 +96,76 @@ __device__ __forceinline__ bool plausible_at(const FrameArgs& a, uint64_t p) {
     return rv == 0 ? (want >= 28 && w5 <= ONC_MAX_AUTH_LEN) : w4 <= 1u;
 }
 
-// 4-bit mask of the zero bytes / high-bit bytes of a dword.
-__device__ __forceinline__ uint32_t zero_nibble(uint32_t w) {
-    const uint32_t z = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);   // 0x80 in each zero byte
-    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
-}
-__device__ __forceinline__ uint32_t high_nibble(uint32_t w) {
-    const uint32_t z = w & 0x80808080u;
-    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
-}
-
-// First position in [c0, c1) whose bytes look like a record start (a guess:
-// correctness never depends on it). 256 positions per step from a 272-byte
-// register window (seventeen aligned 16-byte loads, all in flight together):
-// a record start has its last-fragment bit set and a message type word of 0
-// or 1, i.e. three zero bytes at +8..+10; byte masks of the window select the
-// candidates, and only those get the full test (plausible_at, twice: the
-// candidate and the start its length points to).
-constexpr int kGuessBlocks = 16;              // 16-byte blocks of positions per step
-__device__ __forceinline__ uint64_t guess_start(const FrameArgs& a, uint64_t c0, uint64_t c1) {
-    const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
-    const uint64_t lastblk = (a.len - 1) & ~uint64_t(15);   // last 16-byte block holding a buffer byte
-    const uint64_t hi_pos = min(c1, a.len >= 16 ? a.len - 15 : 0);   // candidates p < hi_pos
-    constexpr int kSub = kGuessBlocks / 4;    // 64-position sub-blocks per step
-    for (uint64_t blk = c0 & ~uint64_t(15); blk < c1; blk += 16 * kGuessBlocks) {
-        uint64_t Z[kSub + 1] = {}, H[kSub] = {};
+// 16-bit mask of the bytes of a 16-byte block (as four dwords) that could
+// start a record: high bit set (last-fragment flag of the record mark) and
+// three zero bytes at +8..+10 (message type 0 or 1 as a big-endian u32).
+// n = the next 16 bytes (for positions whose +8..+10 cross the block).
+__device__ __forceinline__ uint32_t cand_mask16(const u32x4& v, const u32x4& n) {
+    const uint32_t w[8] = {v.x, v.y, v.z, v.w, n.x, n.y, n.z, n.w};
+    uint32_t hi = 0, zero = 0;                // bit k: byte k has the high bit / is zero (k < 32)
 #pragma unroll
-        for (int b = 0; b <= kGuessBlocks; ++b) {
-            const uint64_t o = blk + 16 * b;
-            const u32x4 v = gload<u32x4>(base + (o <= lastblk ? o : lastblk));
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int d = 4 * b + i;             // dword index in the window
-                Z[d >> 4] |= uint64_t(zero_nibble(w[i])) << (4 * (d & 15));
-                if (d < 4 * kGuessBlocks) H[d >> 4] |= uint64_t(high_nibble(w[i])) << (4 * (d & 15));
-            }
-        }
-#pragma unroll
-        for (int sb = 0; sb < kSub; ++sb) {
-            const uint64_t sbase = blk + 64 * sb;
-            // bit k: bytes k+8, k+9, k+10 of the sub-block are zero
-            const uint64_t z8 = (Z[sb] >> 8) | (Z[sb + 1] << 56);
-            const uint64_t z9 = (Z[sb] >> 9) | (Z[sb + 1] << 55);
-            const uint64_t z10 = (Z[sb] >> 10) | (Z[sb + 1] << 54);
-            uint64_t cand = H[sb] & z8 & z9 & z10;
-            const uint64_t lo = c0 > sbase ? c0 - sbase : 0;
-            const uint64_t hi = hi_pos > sbase ? min(uint64_t(64), hi_pos - sbase) : 0;
-            cand &= (hi >= 64 ? ~0ull : ((1ull << hi) - 1)) & (lo >= 64 ? 0ull : ~((1ull << lo) - 1));
-            while (cand) {
-                const uint64_t p = sbase + __ffsll(static_cast<unsigned long long>(cand)) - 1;
-                if (plausible_at(a, p)) {
-                    // and the record it claims is followed by another plausible
-                    // start (or the buffer's end): rejects words inside a record
-                    // that happen to look like a header (e.g. the xid of a
-                    // denied reply, whose next words are 1, 1, 1).
-                    const uint64_t q = p + uint64_t(be_at(base, p) & 0x7FFFFFFFu) + 4;
-                    if (q + 16 > a.len || plausible_at(a, q)) return p;
-                }
-                cand &= cand - 1;
-            }
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t x = w[i];
+        const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);   // 0x80 in each zero byte
+        const uint32_t zb = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+        zero |= zb << (4 * i);
+        if (i < 4) {
+            const uint32_t h = x & 0x80808080u;
+            hi |= (((h >> 7) & 1u) | ((h >> 14) & 2u) | ((h >> 21) & 4u) | ((h >> 28) & 8u)) << (4 * i);
         }
     }
-    return kNone;
+    return hi & (zero >> 8) & (zero >> 9) & (zero >> 10) & 0xFFFFu;
+}
+
+// frame_guess: one wave per chunk t >= 1 (chunk 0 starts at byte 0): the
+// first position in the chunk that looks like a record start, found by a
+// coalesced sweep (lane = 16 positions, 1 KiB of the chunk per step) with
+// the byte-mask filter above, then the full test (plausible_at on the
+// candidate and on the start its length points to) for every candidate of
+// the step in parallel; the lowest passing position wins. A guess only
+// steers the chase: correctness never depends on it. The chunk's chase then
+// runs lane-per-chunk in frame_chunks.
+__global__ __launch_bounds__(256) void frame_guess_kernel(FrameArgs a) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (t >= a.nchunks) return;
+    if (t == 0) {
+        if (lane == 0) a.g[0] = 0;
+        return;
+    }
+    const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
+    const uint64_t c0 = t * a.chunk;
+    const uint64_t c1 = min(c0 + a.chunk, a.len);
+    const uint64_t lastblk = (a.len - 1) & ~uint64_t(15);   // last 16-byte block holding a buffer byte
+    const uint64_t hi_pos = min(c1, a.len >= 16 ? a.len - 15 : 0);   // candidates p < hi_pos
+    uint64_t g = kNone;
+    for (uint64_t blk = c0 & ~uint64_t(15); blk < c1; blk += 1024) {
+        const uint64_t o = blk + 16ull * lane;
+        const u32x4 v = gload<u32x4>(base + (o <= lastblk ? o : lastblk));
+        const u32x4 nx = gload<u32x4>(base + (o + 16 <= lastblk ? o + 16 : lastblk));
+        uint32_t cand = cand_mask16(v, nx);
+        const uint64_t lo = c0 > o ? c0 - o : 0;
+        const uint64_t hi = hi_pos > o ? min(uint64_t(16), hi_pos - o) : 0;
+        cand &= (hi >= 16 ? 0xFFFFu : ((1u << hi) - 1u)) & (lo >= 16 ? 0u : ~((1u << lo) - 1u));
+        uint64_t mine = kNone;
+        while (cand) {
+            const uint64_t p = o + __builtin_ctz(cand);
+            if (plausible_at(a, p)) {
+                const uint64_t q = p + uint64_t(be_at(base, p) & 0x7FFFFFFFu) + 4;
+                if (q + 16 > a.len || plausible_at(a, q)) {
+                    mine = p;
+                    break;
+                }
+            }
+            cand &= cand - 1;
+        }
+        const uint64_t m = __ballot(mine != kNone);
+        if (m) {
+            g = __shfl(mine, __builtin_ctzll(m), 64);
+            break;
+        }
+    }
+    if (lane == 0) a.g[t] = g;
 }
 
 __device__ __forceinline__ void put_chase(const FrameArgs& a, uint64_t t, const Chase& c) {
@@ -176,10 +185,9 @@ __global__ __launch_bounds__(256) void frame_chunks_kernel(FrameArgs a) {
     if (t < ((a.nchunks + 255) >> 8)) a.fail2[t] = a.stop2[t] = 0;
     if (t < ((a.nchunks + 65535) >> 16)) a.fail3[t] = a.stop3[t] = 0;
     if (t >= a.nchunks) return;
-    const uint64_t c0 = t * kFrameChunk;
-    const uint64_t c1 = min(c0 + kFrameChunk, a.len);
-    const uint64_t g = t == 0 ? 0 : guess_start(a, c0, c1);   // chunk 0 starts at byte 0
-    a.g[t] = g;
+    const uint64_t c0 = t * a.chunk;
+    const uint64_t c1 = min(c0 + a.chunk, a.len);
+    const uint64_t g = a.g[t];                 // frame_guess
     if (g == kNone) {
         put_chase(a, t, Chase{kNone, 0, kExit, 0, 0});
         return;
@@ -200,7 +208,7 @@ __global__ __launch_bounds__(256) void frame_verify_kernel(FrameArgs a) {
     if (g != kNone) {
         if (a.st[t] == kExit) {
             const uint64_t x = a.x[t];
-            const uint64_t j = x / kFrameChunk;
+            const uint64_t j = x / a.chunk;
             if (j >= a.nchunks || a.g[j] != x) bad = 1;
             for (uint64_t k = t + 1; k < j && !bad; ++k)
                 if (a.g[k] != kNone) bad = 1;
@@ -294,7 +302,7 @@ __global__ __launch_bounds__(64) void frame_walk_kernel(FrameArgs a) {
         }
         Chase c;
         if (g != E) {
-            c = chase(a, E, min((t + 1) * kFrameChunk, a.len));   // same in every lane
+            c = chase(a, E, min((t + 1) * a.chunk, a.len));   // same in every lane
             if (lane == 0) {
                 a.g[t] = E;
                 put_chase(a, t, c);
@@ -307,7 +315,7 @@ __global__ __launch_bounds__(64) void frame_walk_kernel(FrameArgs a) {
             if (lane == 0) *a.first_stop = t;
             break;
         }
-        const uint64_t j = c.x / kFrameChunk;
+        const uint64_t j = c.x / a.chunk;
         for (uint64_t k = t + 1 + lane; k < j; k += 64) a.g[k] = kNone;
         __threadfence();
         t = j;
@@ -362,9 +370,24 @@ __global__ __launch_bounds__(256) void frame_write_kernel(FrameArgs a) {
 
 hipError_t launch_frame_chunks(const FrameArgs& a, hipStream_t s) {
     const uint32_t blocks = uint32_t((a.nchunks + 255) / 256);
+    hipLaunchKernelGGL(frame_guess_kernel, dim3(uint32_t((a.nchunks + 3) / 4)), dim3(256), 0, s, a);
     hipLaunchKernelGGL(frame_chunks_kernel, dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_verify(const FrameArgs& a, hipStream_t s) {
+    const uint32_t blocks = uint32_t((a.nchunks + 255) / 256);
     hipLaunchKernelGGL(frame_verify_kernel, dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_walk(const FrameArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(frame_walk_kernel, dim3(1), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_counts(const FrameArgs& a, hipStream_t s) {
+    const uint32_t blocks = uint32_t((a.nchunks + 255) / 256);
     hipLaunchKernelGGL(frame_counts_kernel, dim3(blocks), dim3(256), 0, s, a);
     return hipGetLastError();
 }

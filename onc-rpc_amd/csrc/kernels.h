@@ -50,11 +50,12 @@ struct IovArgs {
     uint64_t* block_hdr_base;
 };
 
-constexpr uint64_t kFrameChunk = 4096;   // stream bytes per framing lane
+constexpr uint64_t kFrameChunkDefault = 65536;  // stream bytes per framing lane (FrameArgs::chunk)
 
 struct FrameArgs {
     const uint8_t* wire;
     uint64_t len;
+    uint64_t chunk;         // stream bytes per framing lane
     uint64_t nchunks;
     uint64_t max_records;
     uint64_t* rec_off;      // max_records + 1
@@ -91,6 +92,9 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s);
 hipError_t launch_iov_len(const IovArgs& a, hipStream_t s);
 hipError_t launch_iov_emit(const IovArgs& a, hipStream_t s);
 // frame.hip
+hipError_t launch_frame_verify(const FrameArgs& a, hipStream_t s);
+hipError_t launch_frame_walk(const FrameArgs& a, hipStream_t s);
+hipError_t launch_frame_counts(const FrameArgs& a, hipStream_t s);
 hipError_t launch_frame_chunks(const FrameArgs& a, hipStream_t s);
 hipError_t launch_frame_write(const FrameArgs& a, hipStream_t s);
 // scan.hip

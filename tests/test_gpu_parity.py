@@ -507,7 +507,21 @@ def _frame_both(R, codec, oracle, buf, max_records=None):
     return o
 
 
-def test_frame_stream_valid_streams(codec, R, oracle):
+@pytest.fixture(params=[None, 64, 1024])
+def frame_codec(request, R, monkeypatch):
+    """Codec with the default framing chunk (64 KiB) and with small chunks
+    (ONC_RPC_FRAME_CHUNK), so that test streams span many chunks: guesses,
+    verification and the walk across chunk boundaries."""
+    if request.param is not None:
+        monkeypatch.setenv("ONC_RPC_FRAME_CHUNK", str(request.param))
+    c = R.Codec(0)
+    monkeypatch.delenv("ONC_RPC_FRAME_CHUNK", raising=False)
+    yield c
+    c.close()
+
+
+def test_frame_stream_valid_streams(frame_codec, R, oracle):
+    codec = frame_codec
     for hb in (S.call_none(5000, 256), S.mixed(3000, seed=3, pmin=0, pmax=5000, exotic=0.2),
                L.build_batch(S.random_messages(3000, seed=8, max_payload=300))):
         wire = oracle.encode_batch(hb)[0]
@@ -520,7 +534,8 @@ def test_frame_stream_valid_streams(codec, R, oracle):
             _frame_both(R, codec, oracle, wire, max_records=m)
 
 
-def test_frame_stream_adversarial(codec, R, oracle):
+def test_frame_stream_adversarial(frame_codec, R, oracle):
+    codec = frame_codec
     rng = np.random.default_rng(4)
     # payloads that are themselves RPC streams (nested records fool the guess)
     inner = oracle.encode_batch(S.mixed(400, seed=9, pmin=0, pmax=900))[0]
