@@ -379,7 +379,7 @@ int onc_encode_iov(onc_codec* c, const onc_batch* batch, uint8_t* hdr_out, uint6
 
 // Per-chunk framing state: 56 bytes per chunk + summary flags + the count
 // scan's tile sums.
-static size_t frame_bytes(uint64_t P) { return P * 56 + 2 * (P / 256 + 2) + 2 * (P / 65536 + 2) + (onc::num_tiles(P) + 1) * 16 + 128; }
+static size_t frame_bytes(uint64_t P) { return P * (56 + 8 * 64) + 2 * (P / 256 + 2) + 2 * (P / 65536 + 2) + (onc::num_tiles(P) + 1) * 16 + 128; }
 
 int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* rec_off, uint64_t max_records,
                      uint64_t* result) {
@@ -428,7 +428,8 @@ int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* 
     a.stop2 = flags + (Q / 256 + 2);
     a.fail3 = flags + 2 * (Q / 256 + 2);
     a.stop3 = a.fail3 + (Q / 65536 + 2);
-    uint64_t* tail = reinterpret_cast<uint64_t*>(f + 56 * Q);
+    a.starts = reinterpret_cast<uint64_t*>(f + 56 * Q);    // 64 starts per chunk
+    uint64_t* tail = reinterpret_cast<uint64_t*>(f + (56 + 8 * 64) * Q);
     const uint64_t nt = onc::num_tiles(P);
     uint64_t* tile_sum = tail;
     uint64_t* tile_base = tail + nt + 1;

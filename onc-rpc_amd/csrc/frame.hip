@@ -48,8 +48,26 @@ struct Chase {
     uint32_t aux0, aux1;
 };
 
-// The caller's loop from record start p while p < lim.
-__device__ __forceinline__ Chase chase(const FrameArgs& a, uint64_t p, uint64_t lim) {
+// The caller's loop from record start p while p < lim. The first
+// kStartsCap record starts go to the sink (kept for frame_write, which then
+// copies them instead of chasing again).
+constexpr uint32_t kStartsCap = 64;
+struct NoStarts {
+    __device__ __forceinline__ void operator()(uint32_t, uint64_t) const {}
+};
+struct GlobalStarts {       // straight to the chunk's slice of a.starts (the walk's re-chase)
+    uint64_t* rec;
+    __device__ __forceinline__ void operator()(uint32_t i, uint64_t p) const {
+        if (rec) rec[i] = p;
+    }
+};
+struct LdsStarts {          // chunk-relative u32 in an LDS column (stride 256), copied out after the chase:
+    uint32_t* col;          // a global store inside the chase would hold up the next hop's load (one vmcnt)
+    uint64_t c0;
+    __device__ __forceinline__ void operator()(uint32_t i, uint64_t p) const { col[i * 256] = uint32_t(p - c0); }
+};
+template <class Sink>
+__device__ __forceinline__ Chase chase(const FrameArgs& a, uint64_t p, uint64_t lim, const Sink& rec) {
     const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
     Chase c{p, 0, kExit, 0, 0};
     while (p < lim) {
@@ -69,6 +87,7 @@ __device__ __forceinline__ Chase chase(const FrameArgs& a, uint64_t p, uint64_t 
             c.aux1 = uint32_t(want);
             break;
         }
+        if (c.cnt < kStartsCap) rec(c.cnt, p);
         ++c.cnt;
         p += want;
     }
@@ -177,6 +196,7 @@ __device__ __forceinline__ void put_chase(const FrameArgs& a, uint64_t t, const 
 }
 
 __global__ __launch_bounds__(256) void frame_chunks_kernel(FrameArgs a) {
+    __shared__ uint32_t s_rec[kStartsCap * 256];
     const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (t == 0) {
         *a.first_fail = kNone;
@@ -192,7 +212,10 @@ __global__ __launch_bounds__(256) void frame_chunks_kernel(FrameArgs a) {
         put_chase(a, t, Chase{kNone, 0, kExit, 0, 0});
         return;
     }
-    put_chase(a, t, chase(a, g, c1));
+    const Chase c = chase(a, g, c1, LdsStarts{&s_rec[threadIdx.x], c0});
+    put_chase(a, t, c);
+    uint64_t* rec = a.starts + t * kStartsCap;
+    for (uint32_t i = 0; i < min(c.cnt, kStartsCap); ++i) rec[i] = c0 + s_rec[i * 256 + threadIdx.x];
 }
 
 // fail[t] = 1 when guessed chunk t's chain does not land on a guess, or jumps
@@ -302,7 +325,8 @@ __global__ __launch_bounds__(64) void frame_walk_kernel(FrameArgs a) {
         }
         Chase c;
         if (g != E) {
-            c = chase(a, E, min((t + 1) * a.chunk, a.len));   // same in every lane
+            c = chase(a, E, min((t + 1) * a.chunk, a.len),
+                      GlobalStarts{lane == 0 ? a.starts + t * kStartsCap : nullptr});   // same in every lane
             if (lane == 0) {
                 a.g[t] = E;
                 put_chase(a, t, c);
@@ -348,16 +372,19 @@ __global__ __launch_bounds__(256) void frame_write_kernel(FrameArgs a) {
     const uint64_t k0 = a.cnt_base[t];
     if (ce != 0 && k0 <= a.max_records) {
         const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
+        const uint64_t* rec = a.starts + t * kStartsCap;
+        const bool stored = ce <= kStartsCap;        // the chase kept every start of the chunk
         uint64_t p = a.g[t];
         for (uint32_t i = 0; i < ce; ++i) {
             const uint64_t k = k0 + i;
+            if (stored) p = rec[i];
             if (k == a.max_records) {
                 // capacity: record max_records is not framed; stop before it
                 put_result(a, k, p, ONC_OK, 0, 0);
                 break;
             }
             a.rec_off[k] = p;
-            p += uint64_t(be_at(base, p) & 0x7FFFFFFFu) + 4;
+            if (!stored) p += uint64_t(be_at(base, p) & 0x7FFFFFFFu) + 4;
         }
     }
     if (t == *a.first_stop) {

@@ -59,6 +59,7 @@ struct FrameArgs {
     uint64_t nchunks;
     uint64_t max_records;
     uint64_t* rec_off;      // max_records + 1
+    uint64_t* starts;       // per chunk: its first record starts (frame.hip kStartsCap)
     uint64_t* result;       // [5] n, consumed, status, aux0, aux1
     // per chunk
     uint64_t* g;            // guessed / verified first record start (~0 = none)
