@@ -96,7 +96,7 @@ static void put32(uint8_t* p, uint32_t v) {
 
 int main(int argc, char** argv) {
     const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 1000000;
-    const uint32_t W = 300;
+    const uint32_t W = argc > 2 ? uint32_t(strtoul(argv[2], 0, 10)) : 300;   // record stride (>= 44)
     std::vector<uint8_t> wire(n * W + 64);
     std::vector<uint64_t> off(n + 1);
     for (uint64_t i = 0; i < n; ++i) {
@@ -147,7 +147,7 @@ int main(int argc, char** argv) {
             if (rep >= 5) v.t.push_back(ms * 1000.f);
         }
     }
-    printf("n=%llu cold=%d\n", (unsigned long long)n, int(cold));
+    printf("n=%llu W=%u cold=%d\n", (unsigned long long)n, W, int(cold));
     for (auto& v : vs) {
         std::sort(v.t.begin(), v.t.end());
         printf("%-26s median %7.1f us  min %7.1f\n", v.name, v.t[v.t.size() / 2], v.t[0]);
