@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--mode", choices=["slice", "bytes"], default="slice")
     ap.add_argument("--frame", action="store_true",
                     help="c2: frame the raw stream on the device (onc_frame_stream) instead of scanning rec_len")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pcie-reps", type=int, default=3)
     ap.add_argument("--pcie-chunks", type=int, default=4,

@@ -349,7 +349,10 @@ int32_t onc_expected_message_len(const uint8_t* data, uint64_t len, uint32_t* ou
  *                     ONC_ERR_FRAGMENTED (last-fragment bit clear) or
  *                     ONC_ERR_INCOMPLETE_MESSAGE {aux0 = bytes left,
  *                     aux1 = record length} (wait for more data).
- * SURVEY §8(f) rank 1. */
+ * The stream is cut into 64 KiB chunks framed speculatively in parallel and
+ * verified (frame.hip); ONC_RPC_FRAME_CHUNK (bytes, >= 64) in the
+ * environment at onc_codec_create overrides the chunk size (tests use small
+ * chunks to exercise the multi-chunk logic). SURVEY §8(f) rank 1. */
 int onc_frame_stream(onc_codec* codec, const uint8_t* wire, uint64_t len,
                      uint64_t* rec_off, uint64_t max_records, uint64_t* result);
 
