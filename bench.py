@@ -518,6 +518,7 @@ def main():
         "frame_verify_kernel": 0,
         "frame_walk_kernel": 0,
         "frame_counts_kernel": 0,
+        "frame_guess_kernel": 0,
     }
     kern = {}
     for name, (tot_ms, cnt) in breakdown.items():

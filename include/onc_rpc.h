@@ -259,7 +259,8 @@ int onc_abi_version(void);
 #define ONC_K_FRAME_VERIFY 11
 #define ONC_K_FRAME_WALK   12
 #define ONC_K_FRAME_COUNTS 13
-#define ONC_K_COUNT       14
+#define ONC_K_FRAME_GUESS  14
+#define ONC_K_COUNT       15
 #define ONC_TIMING_ALL    (-1)
 int onc_codec_enable_timing(onc_codec* codec, int enable);
 int onc_codec_kernel_stats(onc_codec* codec, double* ms_total /*[ONC_K_COUNT]*/,

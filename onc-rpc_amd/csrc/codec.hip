@@ -220,6 +220,7 @@ const char* onc_kernel_name(int k) {
         case ONC_K_FRAME_VERIFY: return "frame_verify_kernel";
         case ONC_K_FRAME_WALK: return "frame_walk_kernel";
         case ONC_K_FRAME_COUNTS: return "frame_counts_kernel";
+        case ONC_K_FRAME_GUESS: return "frame_guess_kernel";
         default: return "?";
     }
 }
@@ -435,7 +436,9 @@ int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* 
     uint64_t* tile_base = tail + nt + 1;
     a.first_fail = tail + 2 * (nt + 1);
     a.first_stop = a.first_fail + 1;
-    int rc = run(c, ONC_K_FRAME, "frame_chunks", [&] { return onc::launch_frame_chunks(a, c->stream); });
+    int rc = run(c, ONC_K_FRAME_GUESS, "frame_guess", [&] { return onc::launch_frame_guess(a, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    rc = run(c, ONC_K_FRAME, "frame_chunks", [&] { return onc::launch_frame_chunks(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
     rc = run(c, ONC_K_FRAME_VERIFY, "frame_verify", [&] { return onc::launch_frame_verify(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;

@@ -395,9 +395,13 @@ __global__ __launch_bounds__(256) void frame_write_kernel(FrameArgs a) {
     }
 }
 
+hipError_t launch_frame_guess(const FrameArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(frame_guess_kernel, dim3(uint32_t((a.nchunks + 3) / 4)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_frame_chunks(const FrameArgs& a, hipStream_t s) {
     const uint32_t blocks = uint32_t((a.nchunks + 255) / 256);
-    hipLaunchKernelGGL(frame_guess_kernel, dim3(uint32_t((a.nchunks + 3) / 4)), dim3(256), 0, s, a);
     hipLaunchKernelGGL(frame_chunks_kernel, dim3(blocks), dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -96,6 +96,7 @@ hipError_t launch_iov_emit(const IovArgs& a, hipStream_t s);
 hipError_t launch_frame_verify(const FrameArgs& a, hipStream_t s);
 hipError_t launch_frame_walk(const FrameArgs& a, hipStream_t s);
 hipError_t launch_frame_counts(const FrameArgs& a, hipStream_t s);
+hipError_t launch_frame_guess(const FrameArgs& a, hipStream_t s);
 hipError_t launch_frame_chunks(const FrameArgs& a, hipStream_t s);
 hipError_t launch_frame_write(const FrameArgs& a, hipStream_t s);
 // scan.hip
