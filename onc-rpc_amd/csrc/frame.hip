@@ -102,17 +102,22 @@ __device__ __forceinline__ Chase chase(const FrameArgs& a, uint64_t p, uint64_t 
 // verifier length <= 200, or reply_stat 1 with a rejection kind 0/1. Every
 // record the reference's decoder accepts passes; the test only steers the
 // guess (a record that fails it is still framed, via the walk).
+template <class Be>
+__device__ __forceinline__ bool plausible_with(uint64_t len, uint64_t p, const Be& be) {
+    const uint32_t h = be(0);
+    const uint32_t mt = be(8);
+    const uint32_t rv = be(12);
+    const uint64_t want = uint64_t(h & 0x7FFFFFFFu) + 4;
+    if (!(h & 0x80000000u) || want < 24 || want > len - p) return false;
+    if (mt == 0) return rv == 2u && want >= 44 && be(32) <= ONC_MAX_AUTH_LEN;
+    if (mt != 1 || rv > 1u) return false;
+    const uint32_t w4 = be(16), w5 = be(20);
+    return rv == 0 ? (want >= 28 && w5 <= ONC_MAX_AUTH_LEN) : w4 <= 1u;
+}
+
 __device__ __forceinline__ bool plausible_at(const FrameArgs& a, uint64_t p) {
     const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
-    const uint32_t h = be_at(base, p);
-    const uint32_t mt = be_at(base, p + 8);
-    const uint32_t rv = be_at(base, p + 12);
-    const uint64_t want = uint64_t(h & 0x7FFFFFFFu) + 4;
-    if (!(h & 0x80000000u) || want < 24 || want > a.len - p) return false;
-    if (mt == 0) return rv == 2u && want >= 44 && be_at(base, p + 32) <= ONC_MAX_AUTH_LEN;
-    if (mt != 1 || rv > 1u) return false;
-    const uint32_t w4 = be_at(base, p + 16), w5 = be_at(base, p + 20);
-    return rv == 0 ? (want >= 28 && w5 <= ONC_MAX_AUTH_LEN) : w4 <= 1u;
+    return plausible_with(a.len, p, [&](uint32_t k) { return be_at(base, p + k); });
 }
 
 // 16-bit mask of the bytes of a 16-byte block (as four dwords) that could
@@ -136,55 +141,114 @@ __device__ __forceinline__ uint32_t cand_mask16(const u32x4& v, const u32x4& n) 
     return hi & (zero >> 8) & (zero >> 9) & (zero >> 10) & 0xFFFFu;
 }
 
-// frame_guess: one wave per chunk t >= 1 (chunk 0 starts at byte 0): the
-// first position in the chunk that looks like a record start, found by a
-// coalesced sweep (lane = 16 positions, 1 KiB of the chunk per step) with
-// the byte-mask filter above, then the full test (plausible_at on the
-// candidate and on the start its length points to) for every candidate of
-// the step in parallel; the lowest passing position wins. A guess only
-// steers the chase: correctness never depends on it. The chunk's chase then
-// runs lane-per-chunk in frame_chunks.
+// frame_guess: one wave per kGuessSub consecutive chunks (1 by default;
+// chunk 0 starts at byte 0): for each, the first position in the chunk that
+// looks like a record start. A coalesced sweep (lane = 16 positions, 1 KiB
+// of every chunk per step) stages the step's bytes (+ 64 B of lookahead) in
+// LDS; the byte-mask filter picks candidates, the full test
+// (plausible_with) reads them from LDS, and only candidates that pass it
+// test the start their length points to (global loads, every lane at
+// once); the lowest passing position wins. A guess only steers the chase:
+// correctness never depends on it. Measured on configs[2] (64 KiB chunks):
+// 36 µs; the same sweep testing candidates with global loads 39 µs; four
+// chunks per wave (one step loop over all four) 68 µs — a wave runs until
+// its slowest chunk is found, at 142 VGPRs.
+#ifndef ONC_GUESS_SUB
+#define ONC_GUESS_SUB 1
+#endif
+constexpr int kGuessSub = ONC_GUESS_SUB;
+constexpr int kGuessWin = 272;            // dwords per staged step: 1 KiB + 64 B
 __global__ __launch_bounds__(256) void frame_guess_kernel(FrameArgs a) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
-    if (t >= a.nchunks) return;
-    if (t == 0) {
-        if (lane == 0) a.g[0] = 0;
-        return;
-    }
+    __shared__ uint32_t s_win[4][kGuessSub][kGuessWin];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t t0 = (uint64_t(blockIdx.x) * 4 + wv) * kGuessSub;
+    if (t0 >= a.nchunks) return;
     const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
-    const uint64_t c0 = t * a.chunk;
-    const uint64_t c1 = min(c0 + a.chunk, a.len);
     const uint64_t lastblk = (a.len - 1) & ~uint64_t(15);   // last 16-byte block holding a buffer byte
-    const uint64_t hi_pos = min(c1, a.len >= 16 ? a.len - 15 : 0);   // candidates p < hi_pos
-    uint64_t g = kNone;
-    for (uint64_t blk = c0 & ~uint64_t(15); blk < c1; blk += 1024) {
-        const uint64_t o = blk + 16ull * lane;
-        const u32x4 v = gload<u32x4>(base + (o <= lastblk ? o : lastblk));
-        const u32x4 nx = gload<u32x4>(base + (o + 16 <= lastblk ? o + 16 : lastblk));
-        uint32_t cand = cand_mask16(v, nx);
-        const uint64_t lo = c0 > o ? c0 - o : 0;
-        const uint64_t hi = hi_pos > o ? min(uint64_t(16), hi_pos - o) : 0;
-        cand &= (hi >= 16 ? 0xFFFFu : ((1u << hi) - 1u)) & (lo >= 16 ? 0u : ~((1u << lo) - 1u));
-        uint64_t mine = kNone;
-        while (cand) {
-            const uint64_t p = o + __builtin_ctz(cand);
-            if (plausible_at(a, p)) {
-                const uint64_t q = p + uint64_t(be_at(base, p) & 0x7FFFFFFFu) + 4;
-                if (q + 16 > a.len || plausible_at(a, q)) {
-                    mine = p;
-                    break;
+    uint64_t g[kGuessSub];
+    uint32_t open = 0;                         // bit j: chunk t0 + j still searching
+#pragma unroll
+    for (int j = 0; j < kGuessSub; ++j) {
+        g[j] = kNone;
+        if (t0 + j == 0) g[j] = 0;
+        else if (t0 + j < a.nchunks) open |= 1u << j;
+    }
+    for (uint64_t step = 0; open; ++step) {
+        uint64_t blk[kGuessSub];
+        u32x4 v[kGuessSub], tv[kGuessSub];
+#pragma unroll
+        for (int j = 0; j < kGuessSub; ++j) {
+            const uint64_t c0 = (t0 + j) * a.chunk, c1 = min(c0 + a.chunk, a.len);
+            blk[j] = (c0 & ~uint64_t(15)) + 1024 * step;
+            if ((open >> j) & 1) {
+                if (blk[j] >= c1) {
+                    open &= ~(1u << j);        // no record start in the chunk
+                } else {
+                    const uint64_t o = blk[j] + 16ull * lane;
+                    v[j] = gload<u32x4>(base + (o <= lastblk ? o : lastblk));
+                    const uint64_t ot = blk[j] + 1024 + 16ull * (lane & 3);
+                    if (lane < 4) tv[j] = gload<u32x4>(base + (ot <= lastblk ? ot : lastblk));
                 }
             }
-            cand &= cand - 1;
         }
-        const uint64_t m = __ballot(mine != kNone);
-        if (m) {
-            g = __shfl(mine, __builtin_ctzll(m), 64);
-            break;
+        if (!open) break;
+#pragma unroll
+        for (int j = 0; j < kGuessSub; ++j) {
+            if ((open >> j) & 1) {
+                uint32_t* w = s_win[wv][j];
+                w[4 * lane + 0] = v[j].x; w[4 * lane + 1] = v[j].y; w[4 * lane + 2] = v[j].z; w[4 * lane + 3] = v[j].w;
+                if (lane < 4) {
+                    w[256 + 4 * lane + 0] = tv[j].x; w[256 + 4 * lane + 1] = tv[j].y;
+                    w[256 + 4 * lane + 2] = tv[j].z; w[256 + 4 * lane + 3] = tv[j].w;
+                }
+            }
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int j = 0; j < kGuessSub; ++j) {
+            if (!((open >> j) & 1)) continue;
+            const uint32_t* w = s_win[wv][j];
+            const uint64_t c0 = (t0 + j) * a.chunk, c1 = min(c0 + a.chunk, a.len);
+            const uint64_t hi_pos = min(c1, a.len >= 16 ? a.len - 15 : 0);   // candidates p < hi_pos
+            const uint64_t o = blk[j] + 16ull * lane;
+            const u32x4 nx = {w[4 * lane + 4], w[4 * lane + 5], w[4 * lane + 6], w[4 * lane + 7]};
+            uint32_t cand = cand_mask16(v[j], nx);
+            const uint64_t lo = c0 > o ? c0 - o : 0;
+            const uint64_t hi = hi_pos > o ? min(uint64_t(16), hi_pos - o) : 0;
+            cand &= (hi >= 16 ? 0xFFFFu : ((1u << hi) - 1u)) & (lo >= 16 ? 0u : ~((1u << lo) - 1u));
+            uint64_t mine = kNone;
+            while (cand) {
+                const uint32_t r = 16u * lane + __builtin_ctz(cand);   // window byte offset (< 1024)
+                const uint64_t p = blk[j] + r;
+                const auto be_lds = [&](uint32_t k) {
+                    const uint32_t q = r + k, wi = q >> 2, sh = q & 3u;
+                    return bswap(funnel(w[wi], sh ? w[wi + 1] : 0u, sh));
+                };
+                if (plausible_with(a.len, p, be_lds)) {
+                    // and the record it claims is followed by another
+                    // plausible start (or the buffer's end): rejects words
+                    // inside a record that happen to look like a header
+                    const uint64_t q = p + uint64_t(be_lds(0) & 0x7FFFFFFFu) + 4;
+                    if (q + 16 > a.len || plausible_at(a, q)) {
+                        mine = p;
+                        break;
+                    }
+                }
+                cand &= cand - 1;
+            }
+            const uint64_t m = __ballot(mine != kNone);
+            if (m) {
+                g[j] = __shfl(mine, __builtin_ctzll(m), 64);
+                open &= ~(1u << j);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();       // the next step overwrites the windows
     }
-    if (lane == 0) a.g[t] = g;
+#pragma unroll
+    for (int j = 0; j < kGuessSub; ++j)
+        if (lane == j && t0 + j < a.nchunks) a.g[t0 + j] = g[j];
 }
 
 __device__ __forceinline__ void put_chase(const FrameArgs& a, uint64_t t, const Chase& c) {
@@ -396,7 +460,8 @@ __global__ __launch_bounds__(256) void frame_write_kernel(FrameArgs a) {
 }
 
 hipError_t launch_frame_guess(const FrameArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(frame_guess_kernel, dim3(uint32_t((a.nchunks + 3) / 4)), dim3(256), 0, s, a);
+    const uint64_t waves = (a.nchunks + kGuessSub - 1) / kGuessSub;
+    hipLaunchKernelGGL(frame_guess_kernel, dim3(uint32_t((waves + 3) / 4)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
