@@ -21,7 +21,7 @@ Besides the device-resident `value`, every run also times the PCIe-inclusive
 rate (pinned host inputs -> H2D -> kernels -> D2H of the outputs), reported
 as `pcie_inclusive` (never as `value`).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c2|c3]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c0|c1|c2|c3]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
@@ -35,7 +35,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "device-resident ONC-RPC encode+decode: Mmsgs/s and GiB/s vs HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
-DEFAULT_RECORDS = {"c1": 1_000_000, "c2": 1_000_000, "c3": 4_000_000}
+DEFAULT_RECORDS = {"c0": 1_000_000, "c1": 1_000_000, "c2": 1_000_000, "c3": 4_000_000}
 
 
 def parse():
@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["c1", "c2", "c3"], default="c1")
+    ap.add_argument("--workload", choices=["c0", "c1", "c2", "c3"], default="c1")
     ap.add_argument("--records", type=int, default=None, help="records per GPU")
     ap.add_argument("--mode", choices=["slice", "bytes"], default="slice")
     ap.add_argument("--frame", action="store_true",
@@ -342,6 +342,10 @@ def main():
         hb = S.mixed(n, seed=2 + rank)
         desc = ("configs[2]: mixed Call/Reply (payloads 64..4096 B), " +
                 ("device stream framing" if args.frame else "rec_len scan") + " + decode")
+    elif wl == "c0":
+        hb = S.cpu_roundtrip(n, seed=rank)
+        desc = ("configs[0] message (benches/bench.rs:86-101: Call(AuthUnix 16 gids) + AuthNone + 64 B payload) "
+                "as a batch, encode -> decode")
     else:
         hb = S.call_unix16(n, 1024, seed=3 + rank)
         desc = "configs[3]: Call(AuthUnix 16 gids) + AuthNone + 1 KiB payload, encode -> decode"
