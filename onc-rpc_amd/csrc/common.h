@@ -7,6 +7,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/onc_rpc.h"
@@ -322,17 +323,33 @@ __device__ __forceinline__ void put_auth_words(const onc_auth& a, const EncSrc& 
         for (uint32_t j = 0; 4 * j < len; ++j) out(load4_masked(b + 4ull * j, b + len));
         return;
     }
-    const onc_unix_params* u = s.unix + a.ref;
-    const uint32_t nl = u->name_len, ng = u->ngids;
+    static_assert(sizeof(onc_unix_params) == 96 && offsetof(onc_unix_params, ngids) == 12 &&
+                      offsetof(onc_unix_params, name_off) == 16 && offsetof(onc_unix_params, name_len) == 24 &&
+                      offsetof(onc_unix_params, gids) == 32,
+                  "parameter block layout read below");
+    // the whole 96-byte parameter block in six dwordx4 loads issued together
+    // (one memory round trip; field by field, each gid was a dependent load
+    // between two sink writes)
+    const uintptr_t ua = reinterpret_cast<uintptr_t>(s.unix + a.ref);
+    u32x4 q[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) q[k] = gload<u32x4>(ua + 16 * k);
+    const uint32_t stamp = q[0].x, uid = q[0].y, gid = q[0].z, ng = q[0].w;
+    const uint64_t name_off = uint64_t(q[1].x) | (uint64_t(q[1].y) << 32);
+    const uint32_t nl = q[1].z;
+    const uint32_t gids[ONC_MAX_GIDS] = {q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w,
+                                         q[4].x, q[4].y, q[4].z, q[4].w, q[5].x, q[5].y, q[5].z, q[5].w};
     out(bswap(20u + 4u * words4(nl) + 4u * ng));
-    out(bswap(u->stamp));
+    out(bswap(stamp));
     out(bswap(nl));
-    const uintptr_t b = s.auth_arena + u->name_off;
+    const uintptr_t b = s.auth_arena + name_off;
     for (uint32_t j = 0; 4 * j < nl; ++j) out(load4_masked(b + 4ull * j, b + nl));
-    out(bswap(u->uid));
-    out(bswap(u->gid));
+    out(bswap(uid));
+    out(bswap(gid));
     out(bswap(ng));
-    for (uint32_t j = 0; j < ng; ++j) out(bswap(u->gids[j]));
+#pragma unroll
+    for (uint32_t j = 0; j < ONC_MAX_GIDS; ++j)
+        if (j < ng) out(bswap(gids[j]));
 }
 
 template <class Sink>
