@@ -363,6 +363,8 @@ def test_block_base_scan_path(R, oracle, monkeypatch):
         gpu_vs_oracle_encode(R, c, oracle, hb)
         big = S.call_none(1_100_000, 13, seed=5)       # 1075 workgroups: scan launch, byte path
         gpu_vs_oracle_encode(R, c, oracle, big)
+        edge = S.call_none(1024 * 1024, 8, seed=6)     # exactly 1024 workgroups: the last fused batch
+        gpu_vs_oracle_encode(R, c, oracle, edge)
     finally:
         c.close()
 
