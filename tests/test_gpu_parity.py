@@ -345,6 +345,68 @@ def test_full_size_config1_loopback(codec, R, oracle):
     assert out[lo * 300:hi * 300].cpu().numpy().tobytes() == o_wire
 
 
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_full_size_loopback_idempotent(codec, R, oracle, cfg):
+    """configs[2] (1M mixed Call/Reply, payloads 64..4096 B) and configs[3]
+    (4M Call(AuthUnix 16 gids) + 1 KiB) at full size, with size-independent
+    properties: encode OK and offsets = prefix sum of serialised_len; both
+    decode modes OK with the input xids; serialise(try_from(buf)) == buf over
+    the whole buffer (rpc_message.rs:1150-1153, fuzz parse_serialise.rs:5-12),
+    re-encoding straight from the decoded descriptors (arenas = the wire);
+    plus a 20k-record window bit-exact vs the oracle (encode and decode)."""
+    import torch
+    if cfg == "c2":
+        n, hb = 1_000_000, S.mixed(1_000_000, seed=2)
+    else:
+        n, hb = 4_000_000, S.call_unix16(4_000_000, 1024, seed=3)
+    db = R.DeviceBatch.from_host(hb)
+    rec_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    codec.encode_lengths(db, rec_len, st)
+    codec.sync()
+    lens = rec_len.to(torch.int64)
+    total = int(lens.sum())
+    if cfg == "c3":
+        assert torch.all(lens == 1152)
+    out = torch.empty(total + 16, dtype=torch.uint8, device="cuda")
+    rec_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    codec.encode(db, out, rec_off, st)
+    codec.sync()
+    assert int((st != 0).sum()) == 0
+    assert int(rec_off[0]) == 0 and torch.equal(rec_off[1:], torch.cumsum(lens, 0))
+    del db
+    want_xid = torch.from_numpy(hb.msgs["xid"].view(np.int32).copy()).cuda()
+    bufs = R.DecodeBuffers(n)
+    for mode in MODES:
+        codec.decode(out, rec_off, n, mode, bufs.msgs, bufs.unix, bufs.status, bufs.aux0, bufs.aux1)
+        codec.sync()
+        assert int((bufs.status != 0).sum()) == 0, f"mode {mode}"
+        xid = bufs.msgs.view(-1, 64)[:, 0:4].contiguous().view(torch.int32).view(-1)
+        assert torch.equal(xid, want_xid), f"mode {mode}"
+    # re-encode the decoded batch: descriptors point into the wire itself
+    again = R.DeviceBatch(n, bufs.msgs, bufs.unix, out, out)
+    out2 = torch.empty(total + 16, dtype=torch.uint8, device="cuda")
+    rec_off2 = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    codec.encode(again, out2, rec_off2, st)
+    codec.sync()
+    assert int((st != 0).sum()) == 0
+    assert torch.equal(rec_off2, rec_off)
+    assert torch.equal(out2[:total], out[:total])
+    del out2, again
+    # bit-exact window vs the oracle
+    lo, hi = n // 2, n // 2 + 20_000
+    sub = L.HostBatch(hb.msgs[lo:hi].copy(), hb.unix, hb.auth_arena, hb.payload_arena)
+    o_wire, o_off, o_st, _ = oracle.encode_batch(sub)
+    b0, b1 = int(rec_off[lo]), int(rec_off[hi])
+    g_wire = out[b0:b1].cpu().numpy()
+    assert g_wire.tobytes() == o_wire
+    w = np.concatenate([g_wire, np.zeros(16, np.uint8)])
+    for mode in MODES:
+        g = R.decode_host_wire(codec, w, o_off, mode)
+        o = oracle.decode_batch(w, o_off, mode)
+        assert_decoded_equal(g, o, f"{cfg} window")
+
+
 def test_block_base_scan_path(R, oracle, monkeypatch):
     """Encode places tiles either from enc_emit's own sum of the enc_len
     workgroup totals (<= 1024 workgroups) or from the scan kernel: the
