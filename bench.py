@@ -9,24 +9,37 @@ record of that buffer (src/rpc_message.rs:235-271), inputs resident in HBM.
 
 Workloads (--workload; the default is the headline line):
   c1  configs[1] — 1M Call(prog 100003, vers 4, proc 1, AuthNone(None) x2)
-      + 256 B random payload (W = 300 B), encode -> decode loopback.
+      + 256 B random payload (W = 300 B) per GPU, encode -> decode loopback
+      (weak scaling: every rank its own 1M records).
   c2  configs[2] — 1M mixed Call/Reply, payloads 64..4096 B: decode step =
       scan of rec_len into offsets + decode (input wire encoded once, untimed).
   c3  configs[3] — 4M Call(AuthUnix 16 gids) + 1 KiB payload (W = 1152),
       encode -> decode loopback.
-For --gpus N every rank processes its own shard of --records records per GPU
-(weak scaling, no data-path collective).
+  c0  configs[0]'s message (benches/bench.rs:86-101) as a 1M batch.
+  c4  configs[4] — 64M configs[1] records IN TOTAL, sharded contiguously
+      over the ranks (64M / 32M / 16M / 8M per GPU at 1 / 2 / 4 / 8 GPUs:
+      strong scaling), generated on the device; per-GPU and aggregate
+      Mmsgs/s, every shard's base in the global send buffer from one
+      all_gather of the byte totals (no data-path collective).
+Unless --c4-leg off, a run of c0..c3 also runs the configs[4] leg after the
+headline and reports it as `configs4` in the same JSON line (so the
+driver's 1/2/4/8-GPU runs record configs[4] at every N).
+
+Launch: `python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the
+environment starts N ranks itself (python -m torch.distributed.run, one
+process per GPU, as a child process before any GPU call) and exits with
+their status; under torch.distributed.run (WORLD_SIZE set) every rank
+checks that the world size equals --gpus.
 
 Besides the device-resident `value`, every run also times the PCIe-inclusive
 rate (pinned host inputs -> H2D -> kernels -> D2H of the outputs), reported
 as `pcie_inclusive` (never as `value`).
-
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c0|c1|c2|c3]
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,32 +48,81 @@ sys.path.insert(0, ROOT)
 
 METRIC = "device-resident ONC-RPC encode+decode: Mmsgs/s and GiB/s vs HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
-DEFAULT_RECORDS = {"c0": 1_000_000, "c1": 1_000_000, "c2": 1_000_000, "c3": 4_000_000}
+DEFAULT_RECORDS = {"c0": 1_000_000, "c1": 1_000_000, "c2": 1_000_000, "c3": 4_000_000, "c4": 64_000_000}
+C4_W, C4_H = 300, 44          # configs[4] record: wire bytes / parsed header bytes
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs, one rank each (default: WORLD_SIZE or 1); N > 1 without WORLD_SIZE spawns N ranks")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["c0", "c1", "c2", "c3"], default="c1")
-    ap.add_argument("--records", type=int, default=None, help="records per GPU")
+    ap.add_argument("--workload", choices=["c0", "c1", "c2", "c3", "c4"], default="c1")
+    ap.add_argument("--records", type=int, default=None, help="records per GPU (c0-c3) / in total (c4)")
+    ap.add_argument("--c4-leg", choices=["on", "off"], default="on",
+                    help="also run the configs[4] strong-scaling leg after a c0..c3 headline")
+    ap.add_argument("--c4-records", type=int, default=DEFAULT_RECORDS["c4"], help="configs[4] leg: records in total")
     ap.add_argument("--mode", choices=["slice", "bytes"], default="slice")
     ap.add_argument("--frame", action="store_true",
                     help="c2: frame the raw stream on the device (onc_frame_stream) instead of scanning rec_len")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend of the ranks (control plane only)")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="start the ranks, check the world size and print it; no GPU work (launcher test)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = every core available)")
     ap.add_argument("--pcie-reps", type=int, default=3)
     ap.add_argument("--pcie-chunks", type=int, default=4,
                     help="record chunks of the pipelined PCIe-inclusive leg (two streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
     ap.add_argument("--traffic-json", default=None,
-                    help="per-kernel PMC traffic (default profiles/traffic_r01.json for c1, "
-                         "profiles/traffic_r01_<workload>.json otherwise)")
-    return ap.parse_args()
+                    help="per-kernel PMC traffic (default: the newest profiles/traffic_rNN[_<workload>].json)")
+    return ap.parse_args(argv)
 
 
+# ---------------------------------------------------------------------------
+# launcher
+# ---------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(gpus, argv):
+    """One process per GPU under torch.distributed.run, started as a child
+    (this process never touches the GPU); returns their exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+def check_launch(args, world, rank):
+    """--check-launch: the ranks rendezvous, all_gather (rank, pid) and rank 0
+    prints the world as the process group sees it. No GPU call."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group(args.backend)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+        t = torch.tensor([rank, os.getpid()], dtype=torch.int64)
+        outs = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(outs, t)
+        ranks = [[int(x) for x in o] for o in outs]
+        dist.destroy_process_group()
+    else:
+        ranks = [[0, os.getpid()]]
+    if rank == 0:
+        print(json.dumps({"check_launch": True, "n_gpus": world, "gpus_arg": args.gpus, "ranks": ranks,
+                          "backend": args.backend if world > 1 else None}), flush=True)
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline
+# ---------------------------------------------------------------------------
 def cpu_info():
     model = "unknown"
     try:
@@ -72,6 +134,46 @@ def cpu_info():
     except OSError:
         pass
     return model, os.cpu_count()
+
+
+def cpu_available():
+    """CPUs this process may use: its affinity mask, capped by the cgroup
+    CPU quota (cpu.max) when one is set."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def native_oracle():
+    """The oracle compiled -O3 -march=native for THIS host (BASELINE.md's
+    CPU-baseline build), cached per CPU model/flags under oracle/_native.
+    Returns (path, flags) or (None, reason) when gcc is unavailable."""
+    import hashlib
+    try:
+        with open("/proc/cpuinfo") as f:
+            first = f.read().split("\n\n")[0]
+    except OSError:
+        first = ""
+    key = hashlib.sha1(first.encode()).hexdigest()[:12]
+    d = os.path.join(ROOT, "oracle", "_native", key)
+    so = os.path.join(d, "liboncoracle.so")
+    flags = ["-O3", "-march=native", "-std=c11", "-fPIC", "-shared"]
+    if not os.path.exists(so):
+        os.makedirs(d, exist_ok=True)
+        tmp = so + f".{os.getpid()}"
+        try:
+            subprocess.check_call(["gcc", *flags, "-o", tmp, os.path.join(ROOT, "oracle", "onc_oracle.c"), "-lpthread"])
+            os.replace(tmp, so)
+        except (OSError, subprocess.CalledProcessError) as e:
+            return None, f"native build failed ({e}); prebuilt -O2 oracle used"
+    return so, " ".join(flags)
 
 
 def parsed_bytes(hb, rec_len):
@@ -93,20 +195,25 @@ def parsed_bytes(hb, rec_len):
     return h
 
 
-def cpu_baseline(args, hb, gpu_wire_prefix, wire_np, rec_off_np, mode):
-    """Oracle (C restatement of the reference) on the GPU box's host cores, on
-    a bounded sample of the same workload: `--cpu-threads` threads over the
-    whole batch (contiguous partition), and 1 thread on a 20k-record slice.
-    Also checks a slice of the CPU output against the GPU's bytes."""
+def cpu_baseline(args, wl, hb, gpu_wire_prefix, wire_np, rec_off_np, mode):
+    """Oracle (C restatement of the reference, compiled -O3 -march=native on
+    this host) on the GPU box's host cores, on a bounded sample of the same
+    workload: every available core over whole batches (contiguous record
+    partition), and 1 thread on 20k-record slices. Also checks a slice of
+    the CPU output against the GPU's bytes."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
 
     import oracle_ffi
     import onc_rpc_amd.layout as L
 
+    so, build = native_oracle()
+    if so:
+        oracle_ffi.use_library(so)
     model, ncpu = cpu_info()
-    threads = max(1, min(args.cpu_threads, ncpu or 1))
-    decode_only = args.workload == "c2"
+    avail, affinity, quota = cpu_available()
+    threads = args.cpu_threads if args.cpu_threads > 0 else avail
+    decode_only = wl == "c2"
     chunk = min(20_000, hb.n)
     sub = L.HostBatch(hb.msgs[:chunk].copy(), hb.unix, hb.auth_arena, hb.payload_arena)
     wire, off, st, _ = oracle_ffi.encode_batch(sub)
@@ -148,15 +255,19 @@ def cpu_baseline(args, hb, gpu_wire_prefix, wire_np, rec_off_np, mode):
         "unit": "Mmsgs/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{dn} records ({hb.n}-record batches of the same {args.workload} workload, {what}) in "
-                  f"{en:.1f} s on {threads} threads (contiguous record partition) of a {ncpu}-CPU host ({model})",
+        "sample": f"{dn} records ({hb.n}-record batches of the same {wl} workload, {what}) in "
+                  f"{en:.1f} s on {threads} threads (contiguous record partition) of a {ncpu}-CPU host ({model}); "
+                  f"oracle built {build}",
+        "host_cpus": ncpu, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
         "single_thread": {"value": d1 / e1 / 1e6, "unit": "Mmsgs/s", "cores": 1,
                           "sample": f"{d1} records ({chunk}-record slices) in {e1:.1f} s"},
         "sample_bit_exact_vs_gpu": bool(parity),
     }
 
 
-
+# ---------------------------------------------------------------------------
+# PCIe-inclusive legs
+# ---------------------------------------------------------------------------
 def pcie_pipelined(args, torch, R, wl, hb, db, out, total_bytes, lens_np, rec_len, dec_off, dec, mode, h_in,
                    local_rank, dist, n_total):
     """PCIe-inclusive rate with the copies overlapped: the batch is cut into
@@ -306,33 +417,238 @@ def pcie_pipelined(args, torch, R, wl, hb, db, out, total_bytes, lens_np, rec_le
             "note": "host wall clock; %d record chunks through copy-in / kernel / copy-out streams: H2D, "
                     "kernels and D2H of neighbouring chunks overlap" % K}
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import numpy as np
-    import torch
 
-    import _onc_pkg
+# ---------------------------------------------------------------------------
+# timing + roofline (shared by every workload)
+# ---------------------------------------------------------------------------
+ALG_PER_LAUNCH = {
+    # algorithmic bytes per launch: encode reads ~W and writes
+    # W; zero-copy decode reads H + 4 (the length) and writes ~H.
+    "enc_len_kernel": lambda n, W, H: n * (64 + 4),          # descriptor read + status write
+    "scan_tiles_kernel": lambda n, W, H: 0,
+    "enc_emit_kernel": lambda n, W, H: 2 * W,
+    "decode_kernel": lambda n, W, H: 2 * H + 4 * n,
+    "len_tiles_kernel": lambda n, W, H: 4 * n,
+    "len_apply_kernel": lambda n, W, H: 12 * n,
+    "iov_len_kernel": lambda n, W, H: 0,
+    "iov_emit_kernel": lambda n, W, H: 0,
+    "frame_chunks_kernel": lambda n, W, H: 0,
+    "frame_write_kernel": lambda n, W, H: 8 * n,
+    "frame_verify_kernel": lambda n, W, H: 0,
+    "frame_walk_kernel": lambda n, W, H: 0,
+    "frame_counts_kernel": lambda n, W, H: 0,
+    "frame_guess_kernel": lambda n, W, H: 0,
+}
 
-    _onc_pkg.load()
-    import onc_rpc_amd.layout as L
-    import onc_rpc_amd.runtime as R
-    import onc_rpc_amd.shard as SH
-    import onc_rpc_amd.synth as S
 
-    dist = None
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl")
+class Timing:
+    """W warmup steps; a breakdown pass with every launch bracketed by HIP
+    events (to find the dominant kernel); the timed region: exactly K steps
+    bracketed by barrier + synchronize on both sides, only the dominant
+    kernel's launches bracketed by HIP events on the codec's stream; and an
+    event-free pass of the same K steps."""
+
+    def __init__(self, torch, R, codec, step, steps, warmup, barrier):
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        codec.reset_stats()
+        codec.enable_timing(True)
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        codec.enable_timing(False)
+        self.breakdown = codec.kernel_stats()
+        self.dom_id = max(range(R.K_COUNT),
+                          key=lambda k: self.breakdown[R.K_NAMES[k]][0] / max(1, self.breakdown[R.K_NAMES[k]][1]))
+        codec.reset_stats()
+        codec.enable_timing(True, kernels=[self.dom_id])
+        barrier()
+        torch.cuda.synchronize()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        t_wall0 = time.perf_counter()
+        ev0.record()
+        for _ in range(steps):
+            step()
+        ev1.record()
+        torch.cuda.synchronize()
+        barrier()
+        self.wall_s = time.perf_counter() - t_wall0
+        codec.enable_timing(False)
+        self.ms = ev0.elapsed_time(ev1)
+        self.kstats = codec.kernel_stats()
+        torch.cuda.synchronize()
+        ev2 = torch.cuda.Event(enable_timing=True)
+        ev3 = torch.cuda.Event(enable_timing=True)
+        ev2.record()
+        for _ in range(steps):
+            step()
+        ev3.record()
+        torch.cuda.synchronize()
+        self.ms_clean = ev2.elapsed_time(ev3)
+        self.dom = R.K_NAMES[self.dom_id]
+
+
+def load_traffic(path, wl, n, dom):
+    """HBM bytes per launch of `dom` from the newest PMC traffic file for this
+    workload and batch size (profiles/traffic_rNN[_wl].json), else None."""
+    import glob
+    if path:
+        cands = [path]
+    else:
+        suffix = "" if wl == "c1" else f"_{wl}"
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"traffic_r[0-9][0-9]{suffix}.json")), reverse=True)
+    for p in cands:
+        try:
+            with open(p) as f:
+                tj = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if tj.get("records") == n and tj.get("workload_id", "c1") == wl and dom in tj.get("kernels", {}):
+            return tj["kernels"][dom]["hbm_bytes_per_launch"], os.path.relpath(p, ROOT)
+    return None, None
+
+
+def roofline(tm, n, sum_W, sum_H, step_alg, ms_per_step, traffic, traffic_src):
+    dom_ms, dom_cnt = tm.kstats[tm.dom]
+    dom_us = dom_ms / dom_cnt * 1e3
+    alg = ALG_PER_LAUNCH[tm.dom](n, sum_W, sum_H)
+    achieved = alg / (dom_us * 1e-6) / 1e9
+    step_gbs = step_alg / (ms_per_step / 1e3) / 1e9
+    return {"bound": "hbm", "kernel": tm.dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+            "alg_bytes_per_launch": alg, "avg_launch_us": dom_us, "launches_timed": dom_cnt,
+            # the whole step (every kernel of the metric), per GPU
+            "step_alg_bytes": step_alg, "step_achieved": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS}
+
+
+def breakdown_dict(tm, n, sum_W, sum_H):
+    kern = {}
+    for name, (tot_ms, cnt) in tm.breakdown.items():
+        if cnt:
+            kern[name] = {"avg_us": tot_ms / cnt * 1e3, "launches": cnt,
+                          "alg_bytes_per_launch": ALG_PER_LAUNCH[name](n, sum_W, sum_H)}
+    return kern
+
+
+def gather_per_gpu(torch, dist, dev, rank, n, ms_per_step, ms_clean_per_step):
+    """[records, ms/step, event-free ms/step] of every rank (control plane)."""
+    t = torch.tensor([float(n), ms_per_step, ms_clean_per_step], dtype=torch.float64, device=dev)
+    if dist is None:
+        rows = [t]
+    else:
+        rows = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(rows, t)
+    out = []
+    for r, row in enumerate(rows):
+        nr, ms, msc = (float(x) for x in row.cpu())
+        out.append({"rank": r, "records": int(nr), "ms_per_step": ms, "Mmsgs_per_s": nr / (ms / 1e3) / 1e6,
+                    "ms_per_step_without_kernel_events": msc})
+    return out
+
+
+def agree(torch, dist, dev, ok):
+    """Every rank's flag, AND-ed (one collective all ranks always reach)."""
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+# ---------------------------------------------------------------------------
+# configs[4]: 64M records in total, sharded over the ranks (strong scaling)
+# ---------------------------------------------------------------------------
+def run_c4(args, torch, R, S, SH, L, dist, rank, world, local_rank, total, mode, steps, warmup):
     dev = torch.device("cuda", local_rank)
-    mode = L.DECODE_BYTES if args.mode == "bytes" else L.DECODE_SLICE
-    wl = args.workload
-    per_gpu = args.records or DEFAULT_RECORDS[wl]
+    lo, hi = SH.shard_bounds(total, world, rank)
+    n = hi - lo
+    err = None
+    try:
+        db, gseed = S.call_none_device(lo, hi, 256, seed=4, device=dev)
+        codec = R.Codec(local_rank)
+        codec.reserve(n)
+        local_bytes = n * C4_W
+        out = torch.empty(local_bytes + 16, dtype=torch.uint8, device=dev)
+        rec_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        enc_status = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        dec = R.DecodeBuffers(n, dev)
+        torch.cuda.synchronize()
+    except Exception as e:          # e.g. out of memory: every rank learns it below
+        err = repr(e)
+    if not agree(torch, dist, dev, err is None):
+        return {"error": err or "another rank failed to allocate"}
 
-    n_total = per_gpu * world
+    def step():
+        codec.encode(db, out, rec_off, enc_status)
+        codec.decode(out, rec_off, n, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    tm = Timing(torch, R, codec, step, steps, warmup, barrier)
+    t = torch.tensor([tm.ms, tm.ms_clean], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms_max, ms_clean_max = float(t[0]), float(t[1])
+
+    # validation of the last step (device side) + global placement of the shard
+    ok = int((enc_status[:n] != 0).sum()) == 0 and int((dec.status[:n] != 0).sum()) == 0
+    enc_total = int(rec_off[n]) if n else 0
+    ok = ok and enc_total == local_bytes
+    xid = dec.msgs.view(-1, 64)[:n, 0:4].contiguous().view(torch.int32).view(-1)
+    want = (torch.arange(lo, hi, dtype=torch.int64, device=dev) & 0xFFFFFFFF).to(torch.int32)
+    ok = ok and torch.equal(xid, want)
+    totals = SH.allgather_totals(enc_total) if dist is not None else [enc_total]
+    bases, grand = SH.exclusive_bases(totals)
+    ok = ok and grand == total * C4_W
+    ok = agree(torch, dist, dev, ok)
+
+    per_gpu = gather_per_gpu(torch, dist, dev, rank, n, tm.ms / steps, tm.ms_clean / steps)
+    for r, row in enumerate(per_gpu):
+        row["global_base"] = int(bases[r])
+        row["shard"] = list(SH.shard_bounds(total, world, r))
+    ms_per_step = ms_max / steps
+    sum_W, sum_H = local_bytes, n * C4_H
+    step_alg = 2 * sum_W + 2 * sum_H + 4 * n
+    traffic, tsrc = load_traffic(None, "c4", n, tm.dom)
+    res = {
+        "metric": METRIC, "value": total / (ms_per_step / 1e3) / 1e6, "unit": "Mmsgs/s", "n_gpus": world,
+        "steps": steps, "warmup": warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+        "scaling": "strong", "dtype": "u8",
+        "data": f"synthetic (device RNG, seed {gseed} on rank {rank}): configs[4] records = configs[1]'s "
+                "Call(AuthNone(None) x2) + 256 B",
+        "config": {"workload": f"configs[4]: {total} x 300 B records in total, {n} on rank {rank} "
+                               f"(contiguous shards, {args.mode} mode), encode -> decode, HBM-resident",
+                   "records_total": total, "records_per_gpu": n, "wire_bytes_total": grand,
+                   "parallelism": f"record-sharded x{world} (no collective on the data path)"},
+        "per_gpu": per_gpu,
+        "ms_per_step_without_kernel_events": ms_clean_max / steps,
+        "roofline": roofline(tm, n, sum_W, sum_H, step_alg, ms_per_step, traffic, tsrc),
+        "kernels_breakdown_pass": breakdown_dict(tm, n, sum_W, sum_H),
+        "global_send_buffer": {"shard_bytes": totals, "bases": [int(b) for b in bases], "total": grand,
+                               "note": "exclusive scan of one all_gather'ed int64 per rank "
+                                       "(shard.allgather_totals + exclusive_bases)"},
+        "validated": ok,
+        "wall_s_timed_region": tm.wall_s,
+    }
+    codec.close()
+    del db, out, rec_off, enc_status, dec
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
+
+
+# ---------------------------------------------------------------------------
+# c0..c3
+# ---------------------------------------------------------------------------
+def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
+    import numpy as np
+    dev = torch.device("cuda", local_rank)
+    wl = args.workload
+    per_gpu_n = args.records or DEFAULT_RECORDS[wl]
+    n_total = per_gpu_n * world
     lo, hi = SH.shard_bounds(n_total, world, rank)
     n = hi - lo
     if wl == "c1":
@@ -370,7 +686,6 @@ def main():
         codec.encode(db, out, rec_off, enc_status, rec_len)     # input wire (untimed)
         torch.cuda.synchronize()
         dec_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
-
         frame_res = torch.zeros(5, dtype=torch.int64, device=dev)
 
         def step():
@@ -388,54 +703,8 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    # Breakdown pass (untimed for `value`): every launch bracketed by HIP
-    # events, to find the dominant kernel and report the per-kernel split.
-    codec.reset_stats()
-    codec.enable_timing(True)
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    codec.enable_timing(False)
-    breakdown = codec.kernel_stats()
-    dom_id = max(range(R.K_COUNT), key=lambda k: breakdown[R.K_NAMES[k]][0] / max(1, breakdown[R.K_NAMES[k]][1]))
-
-    # Timed region: exactly K steps, barrier + sync on both sides. Only the
-    # dominant kernel's launches are bracketed by HIP events (on the codec's
-    # stream = torch's current stream) for the roofline.
-    codec.reset_stats()
-    codec.enable_timing(True, kernels=[dom_id])
-    barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t_wall0 = time.perf_counter()
-    ev0.record()
-    for _ in range(args.steps):
-        step()
-    ev1.record()
-    torch.cuda.synchronize()
-    barrier()
-    t_wall = time.perf_counter() - t_wall0
-    codec.enable_timing(False)
-    ms = ev0.elapsed_time(ev1)
-    kstats = codec.kernel_stats()
-
-    # Second, event-free pass of the same K steps (reported for comparison).
-    torch.cuda.synchronize()
-    ev2 = torch.cuda.Event(enable_timing=True)
-    ev3 = torch.cuda.Event(enable_timing=True)
-    ev2.record()
-    for _ in range(args.steps):
-        step()
-    ev3.record()
-    torch.cuda.synchronize()
-    ms_clean = ev2.elapsed_time(ev3)
-
-    t = torch.tensor([ms, ms_clean], dtype=torch.float64, device=dev)
+    tm = Timing(torch, R, codec, step, args.steps, args.warmup, barrier)
+    t = torch.tensor([tm.ms, tm.ms_clean], dtype=torch.float64, device=dev)
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ms_max, ms_clean_max = float(t[0]), float(t[1])
@@ -452,10 +721,10 @@ def main():
     want_xid = torch.from_numpy(hb.msgs["xid"].view(np.int32).copy()).to(dev)
     if not torch.equal(xid, want_xid):
         ok = False
-    okt = torch.tensor([1 if ok else 0], device=dev)
-    if dist is not None:
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-    ok = bool(okt.item())
+    # global placement of this rank's shard in the job's send buffer
+    totals = SH.allgather_totals(int(dec_off[n])) if dist is not None else [int(dec_off[n])]
+    bases, grand = SH.exclusive_bases(totals)
+    ok = agree(torch, dist, dev, ok)
 
     # PCIe-inclusive rate: pinned host inputs -> H2D -> step -> D2H outputs.
     pcie = None
@@ -503,51 +772,11 @@ def main():
     ms_per_step = ms_max / steps
     value = n_total / (ms_per_step / 1e3) / 1e6       # whole-job Mmsgs/s
     wire_gibs = sum_W * world / (ms_per_step / 1e3) / 2**30
-
-    # Roofline of the dominant kernel (per-launch averages from HIP events).
-    # Algorithmic bytes per launch, SURVEY §8(d): encode reads ~W and writes
-    # W; zero-copy decode reads H + 4 (the length) and writes ~H.
-    alg_bytes = {
-        "enc_len_kernel": n * (64 + 4),          # descriptor read + status write
-        "scan_tiles_kernel": 0,
-        "enc_emit_kernel": 2 * sum_W,
-        "decode_kernel": 2 * sum_H + 4 * n,
-        "len_tiles_kernel": 4 * n,
-        "len_apply_kernel": 12 * n,
-        "enc_fixup_kernel": 0,                   # deferred tiles only
-        "iov_len_kernel": 0,
-        "iov_emit_kernel": 0,
-        "frame_chunks_kernel": 0,
-        "frame_write_kernel": 8 * n,
-        "frame_verify_kernel": 0,
-        "frame_walk_kernel": 0,
-        "frame_counts_kernel": 0,
-        "frame_guess_kernel": 0,
-    }
-    kern = {}
-    for name, (tot_ms, cnt) in breakdown.items():
-        if cnt:
-            kern[name] = {"avg_us": tot_ms / cnt * 1e3, "launches": cnt,
-                          "alg_bytes_per_launch": alg_bytes[name]}
-    dom = R.K_NAMES[dom_id]
-    dom_ms, dom_cnt = kstats[dom]
-    dom_us = dom_ms / dom_cnt * 1e3
-    alg = alg_bytes[dom]
-    achieved = alg / (dom_us * 1e-6) / 1e9
-    traffic = None
-    try:
-        tpath = args.traffic_json or os.path.join(
-            ROOT, "profiles", "traffic_r01.json" if wl == "c1" else f"traffic_r01_{wl}.json")
-        with open(tpath) as f:
-            tj = json.load(f)
-        if tj.get("records") == n and tj.get("workload_id", "c1") == wl and dom in tj.get("kernels", {}):
-            traffic = tj["kernels"][dom]["hbm_bytes_per_launch"]
-    except (OSError, ValueError):
-        pass
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "alg_bytes_per_launch": alg, "avg_launch_us": dom_us, "launches_timed": dom_cnt}
     step_alg = (2 * sum_H + 4 * n) + (0 if wl == "c2" else 2 * sum_W)
+    traffic, tsrc = load_traffic(args.traffic_json, wl, n, tm.dom)
+    per_gpu = gather_per_gpu(torch, dist, dev, rank, n, tm.ms / steps, tm.ms_clean / steps)
+    for r, row in enumerate(per_gpu):
+        row["global_base"] = int(bases[r])
     result = {
         "metric": METRIC,
         "value": value,
@@ -568,22 +797,77 @@ def main():
         "wire_GiB_per_s": wire_gibs,
         "ms_per_step_without_kernel_events": ms_clean_max / steps,
         "step_alg_GBs": step_alg * world / (ms_per_step / 1e3) / 1e9,
-        "roofline": roofline,
-        "kernels_breakdown_pass": kern,
+        "roofline": roofline(tm, n, sum_W, sum_H, step_alg, ms_per_step, traffic, tsrc),
+        "per_gpu": per_gpu,
+        "global_send_buffer": {"shard_bytes": totals, "bases": [int(b) for b in bases], "total": grand},
+        "kernels_breakdown_pass": breakdown_dict(tm, n, sum_W, sum_H),
         "pcie_inclusive": pcie,
         "validated": ok,
-        "wall_s_timed_region": t_wall,
+        "wall_s_timed_region": tm.wall_s,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         prefix = out[: min(total_bytes, 20_000 * 4300)].cpu().numpy().tobytes()
         wire_np = out.cpu().numpy()
         off_np = dec_off.cpu().numpy().view(np.uint64)
-        result["cpu_baseline"] = cpu_baseline(args, hb, prefix, wire_np, off_np, mode)
+        result["cpu_baseline"] = cpu_baseline(args, wl, hb, prefix, wire_np, off_np, mode)
     elif rank == 0:
         result["cpu_baseline"] = None
+    codec.close()
+    del db, out, rec_off, dec_off, dec, enc_status, rec_len
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return result
+
+
+def main():
+    args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and (args.gpus or 1) > 1:
+        # one process per GPU, started before this process touches the GPU
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = int(world_env or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is None:
+        args.gpus = world
+    if args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.check_launch:
+        check_launch(args, world, rank)
+        return
+
+    import torch
+
+    import _onc_pkg
+
+    _onc_pkg.load()
+    import onc_rpc_amd.layout as L
+    import onc_rpc_amd.runtime as R
+    import onc_rpc_amd.shard as SH
+    import onc_rpc_amd.synth as S
+
+    dist = None
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(args.backend)
+        if dist.get_world_size() != args.gpus:
+            sys.exit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    mode = L.DECODE_BYTES if args.mode == "bytes" else L.DECODE_SLICE
+
+    if args.workload == "c4":
+        result = run_c4(args, torch, R, S, SH, L, dist, rank, world, local_rank,
+                        args.records or DEFAULT_RECORDS["c4"], mode, args.steps, args.warmup)
+        result["vs_baseline"] = None
+        ok = result.get("validated", False)
+    else:
+        result = run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode)
+        ok = result["validated"]
+        if args.c4_leg == "on":
+            result["configs4"] = run_c4(args, torch, R, S, SH, L, dist, rank, world, local_rank,
+                                        args.c4_records, mode, args.steps, args.warmup)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    codec.close()
     if dist is not None:
         dist.destroy_process_group()
     if not ok:

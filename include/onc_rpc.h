@@ -40,7 +40,9 @@
 extern "C" {
 #endif
 
-#define ONC_RPC_ABI_VERSION 1
+/* 2: onc_batch carries arena sizes (bounds-checked descriptors), onc_encode
+ *    accepts any output address, retired kernel id ONC_K_ENC_FIXUP removed. */
+#define ONC_RPC_ABI_VERSION 2
 
 /* ------------------------------------------------------------------------ */
 /* Wire discriminants (values are the on-wire u32s)                          */
@@ -192,13 +194,25 @@ typedef struct onc_unix_params {
 } onc_unix_params;
 
 /* A batch of messages to encode. [dev] pointers. auth_arena and
- * payload_arena may alias (e.g. both = the wire buffer of a decoded batch). */
+ * payload_arena may alias (e.g. both = the wire buffer of a decoded batch).
+ * The three sizes bound every reference a descriptor makes: a unix-table
+ * index >= unix_count, an auth body / machine name [off, off + len) beyond
+ * auth_len or a payload beyond payload_len makes that record
+ * ONC_ENC_BAD_DESCRIPTOR (checked before anything is read through it), so a
+ * malformed descriptor can never make a kernel read outside the arenas.
+ * Zero-length bodies and payloads are not checked (their offsets are never
+ * dereferenced). The reference's owned types cannot express such a
+ * reference; the check replaces an out-of-bounds read, not a reference
+ * behaviour. */
 typedef struct onc_batch {
     uint64_t               n;
     const onc_msg*         msgs;          /* [dev] n descriptors */
-    const onc_unix_params* unix_params;   /* [dev] AUTH_UNIX table (may be NULL if unused) */
+    const onc_unix_params* unix_params;   /* [dev] AUTH_UNIX table (may be NULL if unix_count == 0) */
     const uint8_t*         auth_arena;    /* [dev] auth bodies + machine names */
     const uint8_t*         payload_arena; /* [dev] payloads */
+    uint64_t               unix_count;    /* entries in unix_params */
+    uint64_t               auth_len;      /* bytes in auth_arena */
+    uint64_t               payload_len;   /* bytes in payload_arena */
 } onc_batch;
 
 /* Decode outputs. [dev] pointers.
@@ -245,22 +259,21 @@ int onc_abi_version(void);
  * stream; the accumulated device time and launch count per kernel id are
  * returned by onc_codec_kernel_stats after a sync. Timing only the kernel
  * of interest keeps the event overhead off the other launches. */
-#define ONC_K_ENC_LEN     0
-#define ONC_K_SCAN_TILES  1
-#define ONC_K_ENC_EMIT    2
-#define ONC_K_DEC_PARSE   3
-#define ONC_K_LEN_TILES   4
-#define ONC_K_LEN_APPLY   5
-#define ONC_K_ENC_FIXUP   6   /* retired: enc_emit handles every tile; never launched */
-#define ONC_K_IOV_LEN     7
-#define ONC_K_IOV_EMIT    8
-#define ONC_K_FRAME       9
-#define ONC_K_FRAME_WRITE 10
-#define ONC_K_FRAME_VERIFY 11
-#define ONC_K_FRAME_WALK   12
-#define ONC_K_FRAME_COUNTS 13
-#define ONC_K_FRAME_GUESS  14
-#define ONC_K_COUNT       15
+#define ONC_K_ENC_LEN      0
+#define ONC_K_SCAN_TILES   1
+#define ONC_K_ENC_EMIT     2
+#define ONC_K_DEC_PARSE    3
+#define ONC_K_LEN_TILES    4
+#define ONC_K_LEN_APPLY    5
+#define ONC_K_IOV_LEN      6
+#define ONC_K_IOV_EMIT     7
+#define ONC_K_FRAME        8
+#define ONC_K_FRAME_WRITE  9
+#define ONC_K_FRAME_VERIFY 10
+#define ONC_K_FRAME_WALK   11
+#define ONC_K_FRAME_COUNTS 12
+#define ONC_K_FRAME_GUESS  13
+#define ONC_K_COUNT        14
 #define ONC_TIMING_ALL    (-1)
 int onc_codec_enable_timing(onc_codec* codec, int enable);
 int onc_codec_kernel_stats(onc_codec* codec, double* ms_total /*[ONC_K_COUNT]*/,
@@ -279,10 +292,15 @@ const char* onc_kernel_name(int kernel_id);
 int onc_encode_lengths(onc_codec* codec, const onc_batch* batch,
                        uint32_t* rec_len, int32_t* status);
 
-/* Encode every record back to back into out[dev] (16-byte aligned,
- * out_cap bytes): the batch equivalent of calling serialise_into for each
- * message in order on one Cursor<Vec<u8>> (a TCP send buffer).
- *   rec_off[dev, n+1]: record i occupies [rec_off[i], rec_off[i+1]);
+/* Encode every record back to back into out[dev] (out_cap bytes): the
+ * batch equivalent of calling serialise_into for each message in order on
+ * one Cursor<Vec<u8>> (a TCP send buffer). `out` may be any byte address —
+ * the cursor's current position in a partly filled buffer — and bytes
+ * before `out` or at/after out + out_cap are never written (the reference
+ * writes at the writer's position, rpc_message.rs:136, and reuses buffers,
+ * README.md:11). Whole 16-byte-aligned chunks are written with one store;
+ * the chunks at either end of the batch are written byte by byte.
+ *   rec_off[dev, n+1]: record i occupies out[rec_off[i], rec_off[i+1]);
  *                      rec_off[n] is the total byte count.
  *   status[dev, n]   : ONC_OK or ONC_ENC_*. Records that fail validation
  *                      occupy 0 bytes. Bytes at or beyond out_cap are never
@@ -324,7 +342,13 @@ int onc_encode_iov(onc_codec* codec, const onc_batch* batch,
 
 /* Decode record i = wire[rec_off[i] .. rec_off[i+1]) for i < n, each
  * exactly as the reference decodes one buffer that must hold exactly one
- * message (src/rpc_message.rs:238-242). mode = ONC_DECODE_SLICE | _BYTES. */
+ * message (src/rpc_message.rs:238-242). mode = ONC_DECODE_SLICE | _BYTES.
+ * Memory access: the decoder reads its records' header bytes as whole
+ * 16-byte-aligned granules (one dwordx4 per granule), so it may read up to
+ * 15 bytes before rec_off[i] / after rec_off[i+1] — never outside the
+ * aligned 16-byte granules that hold record bytes, so never across a page
+ * or allocation boundary of a hipMalloc'd buffer. Those bytes never affect
+ * the result; no byte of the wire is written. */
 int onc_decode(onc_codec* codec, const uint8_t* wire, const uint64_t* rec_off,
                uint64_t n, int mode, const onc_decoded* out);
 

@@ -645,6 +645,9 @@ inline void BatchEncoder::upload(onc_batch& b) {
     b.unix_params = static_cast<const onc_unix_params*>(d_unix_.ensure(unix_.size() * sizeof(onc_unix_params)));
     b.auth_arena = static_cast<const uint8_t*>(d_auth_.ensure(auth_.size() + 16));
     b.payload_arena = static_cast<const uint8_t*>(d_payload_.ensure(payload_.size() + 16));
+    b.unix_count = unix_.size();
+    b.auth_len = auth_.size();
+    b.payload_len = payload_.size();
     if (n) hip_check(hipMemcpy(d_msgs_.as<void>(), msgs_.data(), n * sizeof(onc_msg), hipMemcpyHostToDevice), "H2D");
     if (!unix_.empty())
         hip_check(hipMemcpy(d_unix_.as<void>(), unix_.data(), unix_.size() * sizeof(onc_unix_params),

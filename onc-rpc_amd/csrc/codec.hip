@@ -212,7 +212,6 @@ const char* onc_kernel_name(int k) {
         case ONC_K_DEC_PARSE: return "decode_kernel";
         case ONC_K_LEN_TILES: return "len_tiles_kernel";
         case ONC_K_LEN_APPLY: return "len_apply_kernel";
-        case ONC_K_ENC_FIXUP: return "enc_fixup_kernel (retired)";
         case ONC_K_IOV_LEN: return "iov_len_kernel";
         case ONC_K_IOV_EMIT: return "iov_emit_kernel";
         case ONC_K_FRAME: return "frame_chunks_kernel";
@@ -268,8 +267,14 @@ int onc_codec_reset_stats(onc_codec* c) {
 static int check_batch(const onc_batch* b) {
     if (!b) return ONC_RC_EINVAL;
     if (b->n && !b->msgs) return ONC_RC_EINVAL;
+    // a non-empty arena needs a pointer
+    if ((b->unix_count && !b->unix_params) || (b->auth_len && !b->auth_arena) ||
+        (b->payload_len && !b->payload_arena))
+        return ONC_RC_EINVAL;
     return ONC_RC_OK;
 }
+
+static onc::Bounds bounds_of(const onc_batch* b) { return onc::Bounds{b->unix_count, b->auth_len, b->payload_len}; }
 
 int onc_encode_lengths(onc_codec* c, const onc_batch* batch, uint32_t* rec_len, int32_t* status) {
     if (!c || check_batch(batch) != ONC_RC_OK || (batch->n && (!rec_len || !status))) return ONC_RC_EINVAL;
@@ -284,6 +289,7 @@ int onc_encode_lengths(onc_codec* c, const onc_batch* batch, uint32_t* rec_len, 
     a.unix = batch->unix_params;
     a.auth_arena = batch->auth_arena;
     a.payload_arena = batch->payload_arena;
+    a.bounds = bounds_of(batch);
     a.status = status;
     a.rec_len = rec_len;
     bind_scratch(c, a);
@@ -294,7 +300,6 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
                int32_t* status, uint32_t* rec_len) {
     if (!c || check_batch(batch) != ONC_RC_OK || !rec_off) return ONC_RC_EINVAL;
     if (batch->n && (!status || (!out && out_cap))) return ONC_RC_EINVAL;
-    if ((reinterpret_cast<uintptr_t>(out) & 15) != 0) return ONC_RC_EALIGN;
     if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
     if (batch->n == 0) {
         const hipError_t e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
@@ -309,8 +314,12 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
     a.unix = batch->unix_params;
     a.auth_arena = batch->auth_arena;
     a.payload_arena = batch->payload_arena;
-    a.out = out;
-    a.out_cap = out ? out_cap : 0;
+    a.bounds = bounds_of(batch);
+    // any writer position: the kernels work on 16-byte chunks from the
+    // aligned address below `out`, whose first `origin` bytes are never written
+    a.origin = reinterpret_cast<uintptr_t>(out) & 15;
+    a.out = out - a.origin;
+    a.out_cap = out ? a.origin + out_cap : 0;
     a.rec_off = rec_off;
     a.status = status;
     a.rec_len = rec_len;
@@ -354,6 +363,7 @@ int onc_encode_iov(onc_codec* c, const onc_batch* batch, uint8_t* hdr_out, uint6
     a.unix = batch->unix_params;
     a.auth_arena = batch->auth_arena;
     a.payload_arena = batch->payload_arena;
+    a.bounds = bounds_of(batch);
     a.hdr_out = hdr_out;
     a.hdr_cap = hdr_out ? hdr_cap : 0;
     a.iov = iov;

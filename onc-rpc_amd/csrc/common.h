@@ -119,21 +119,41 @@ struct AuthPlan {
     int32_t status;    // construction-time panics
 };
 
-__device__ __forceinline__ AuthPlan plan_auth(const onc_auth& a, const onc_unix_params* unix) {
+// Sizes of the arenas a batch's descriptors point into (onc_batch): every
+// reference is checked against them before it is dereferenced.
+struct Bounds {
+    uint64_t n_unix;
+    uint64_t auth_len;
+    uint64_t payload_len;
+};
+
+// [off, off + len) lies inside an arena of `size` bytes (no overflow).
+__device__ __forceinline__ bool in_arena(uint64_t off, uint64_t len, uint64_t size) {
+    return off <= size && len <= size - off;
+}
+
+__device__ __forceinline__ AuthPlan plan_auth(const onc_auth& a, const onc_unix_params* unix, const Bounds& bd) {
     AuthPlan p;
     const uint32_t kind = a.kind_len >> 24;
     const uint32_t len = a.kind_len & 0xFFFFFFu;
     p.status = ONC_OK;
     if (kind == ONC_KIND_UNIX) {
+        if (a.ref >= bd.n_unix) { p.status = ONC_ENC_BAD_DESCRIPTOR; p.words = 0; p.assoc = 0; return p; }
         const onc_unix_params* u = unix + a.ref;
         const uint32_t nl = u->name_len, ng = u->ngids;
         // AuthUnixParams::new panics (unix_params.rs:149), then Gids (:47)
         if (nl > ONC_MAX_MACHINE_NAME_LEN) { p.status = ONC_ENC_NAME_GT_255; p.words = 0; p.assoc = 0; return p; }
         if (ng > ONC_MAX_GIDS) { p.status = ONC_ENC_GIDS_GT_16; p.words = 0; p.assoc = 0; return p; }
+        if (nl != 0 && !in_arena(u->name_off, nl, bd.auth_len)) {
+            p.status = ONC_ENC_BAD_DESCRIPTOR; p.words = 0; p.assoc = 0; return p;
+        }
         // id + len + stamp + opaque(name) + uid + gid + ngids + gids
         p.words = 2 + 1 + 1 + words4(nl) + 3 + ng;
         p.assoc = 12 + nl + 4 * ng;               // unix_params.rs:234-245
     } else if (kind <= ONC_KIND_UNKNOWN) {
+        if (len != 0 && !in_arena(a.ref, len, bd.auth_len)) {
+            p.status = ONC_ENC_BAD_DESCRIPTOR; p.words = 0; p.assoc = 0; return p;
+        }
         p.words = 2 + words4(len);                // id + opaque
         p.assoc = len;
     } else {
@@ -157,7 +177,7 @@ __device__ __forceinline__ uint32_t meta_hw(uint32_t m) { return m >> 16; }
 // serialise_into in reference order: descriptor / construction panics
 // (cred, then verf), oversize (rpc_message.rs:146-151), then the
 // associated-data assert (flavor.rs:110, cred before verf).
-__device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_params* unix) {
+__device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_params* unix, const Bounds& bd) {
     RecPlan r;
     r.len = 0;
     r.meta = 0;
@@ -166,9 +186,9 @@ __device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_
     uint64_t body = 0;
     uint32_t assoc_c = 0, assoc_v = 0;
     if (d.msg_type == ONC_MSG_CALL) {
-        AuthPlan c = plan_auth(d.cred, unix);
+        AuthPlan c = plan_auth(d.cred, unix, bd);
         if (c.status) { r.status = c.status; return r; }
-        AuthPlan v = plan_auth(d.verf, unix);
+        AuthPlan v = plan_auth(d.verf, unix, bd);
         if (v.status) { r.status = v.status; return r; }
         cw = c.words; vw = v.words;
         assoc_c = c.assoc; assoc_v = v.assoc;
@@ -177,7 +197,7 @@ __device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_
     } else if (d.msg_type == ONC_MSG_REPLY) {
         if (d.reply_stat == ONC_REPLY_ACCEPTED) {
             if (d.stat > ONC_ACCEPT_SYSTEM_ERR) { r.status = ONC_ENC_BAD_DESCRIPTOR; return r; }
-            AuthPlan v = plan_auth(d.verf, unix);
+            AuthPlan v = plan_auth(d.verf, unix, bd);
             if (v.status) { r.status = v.status; return r; }
             vw = v.words; assoc_v = v.assoc;
             // mark, xid, mtype, reply_stat, verf, accept_stat [, low, high]
@@ -195,6 +215,8 @@ __device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_
     } else {
         r.status = ONC_ENC_BAD_DESCRIPTOR; return r;
     }
+    // payload reference inside the payload arena (onc_batch bounds)
+    if (body != 0 && !in_arena(d.payload_off, body, bd.payload_len)) { r.status = ONC_ENC_BAD_DESCRIPTOR; return r; }
     const uint64_t total = 4ull * hw + body;
     if (total & 0xFFFFFFFF80000000ull) { r.status = ONC_ENC_TOO_LONG; return r; }
     if (assoc_c > ONC_MAX_AUTH_LEN || assoc_v > ONC_MAX_AUTH_LEN) { r.status = ONC_ENC_AUTH_GT_200; return r; }

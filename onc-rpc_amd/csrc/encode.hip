@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kLenThreads) void enc_len_kernel(EncArgs a) {
         const uint64_t r = rw + 64 * k + lane;
         uint64_t len = 0;
         if (r < a.n) {
-            const RecPlan p = plan_record(d[k], a.unix);
+            const RecPlan p = plan_record(d[k], a.unix, a.bounds);
             len = p.len;
             a.status[r] = p.status;
             if (a.rec_len) a.rec_len[r] = uint32_t(len);
@@ -175,9 +175,15 @@ constexpr int kMap2Cap = ONC_MAP_CAP;         // granules per span (granule = 4 
 constexpr int kEmitChunkUnroll = ONC_EMIT_U;    // chunks per lane per pipelined step
 constexpr int kEmitNT = 2;                    // nontemporal output stores (loads: measured slower)
 constexpr uint64_t kSpanBytesMax = 1ull << 30;  // a span's offsets fit uint32 (one record may exceed it)
-// a record's own non-pure chunks: header <= 4 * (7 + 2 * 52) bytes, + the
-// chunk it shares with its predecessor, + its tail chunk
-static_assert((4 * (7 + 2 * 52) + 15) / 16 + 2 <= kImgChunks / 8, "a span of 8 maximal records must fit");
+// A record's own non-pure chunks: its header is at most 4 * (7 + 2 * 54)
+// = 460 bytes (a Call whose cred and verifier are both AUTH_UNIX at the
+// associated-data limit of 200 bytes: 2 + 1 + 1 + 47 + 3 words for a
+// 188-byte name and no gids, or 2 + 1 + 1 + 31 + 3 + 16 for a 124-byte name
+// and 16 gids), a payload under 16 bytes joins it in the image (<= 475
+// bytes), and the header can start and end inside a chunk: <= 31 chunks.
+// Spans are cut at run time to what fits the image (the loop below), so the
+// only static requirement is that one maximal record always fits on its own.
+static_assert((4 * (7 + 2 * 54) + 15 + 15) / 16 + 1 <= kImgChunks, "one maximal record must fit the image");
 
 struct ImgTile {
     uint4 img[kImgChunks];           // assembled non-pure chunks (header bytes; small payloads)
@@ -393,13 +399,15 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         asm volatile("" : "+v"(mr.q[0]), "+v"(mr.q[1]), "+v"(mr.q[2]), "+v"(mr.q[3]), "+v"(tl.v), "+v"(tl.w[0]));
     }
     const onc_msg dm = as_msg(mr);
-    const uint64_t T0 = tile_reduce<kFused>(tl, tile);
+    // output coordinates: byte 0 = the 16-aligned chunk base below the
+    // caller's `out`, which sits at `origin` (any writer position)
+    const uint64_t T0 = a.origin + tile_reduce<kFused>(tl, tile);
     uint64_t len = 0, poff = 0;
     uint32_t hw = 0;
     bool word_aligned = true;
     if (lane < nrec) {
         const onc_msg& d = dm;
-        const RecPlan p = plan_record(d, a.unix);   // the same function as enc_len: lengths agree
+        const RecPlan p = plan_record(d, a.unix, a.bounds);   // the same function as enc_len: lengths agree
         len = p.len;
         hw = len ? meta_hw(p.meta) : 0;
         poff = d.payload_off;
@@ -410,8 +418,8 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     const uint64_t en = start + len;
     const uint64_t pst = start + 4ull * hw;
     if (lane < nrec) {
-        a.rec_off[r0 + lane] = start;
-        if (r0 + lane + 1 == a.n) a.rec_off[a.n] = en;      // the grand total
+        a.rec_off[r0 + lane] = start - a.origin;
+        if (r0 + lane + 1 == a.n) a.rec_off[a.n] = en - a.origin;   // the grand total
         if (len != 0 && en > a.out_cap) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
     }
     const bool byte_mode = !(__all(word_aligned) && (T0 & 3) == 0);

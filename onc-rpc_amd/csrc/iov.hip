@@ -28,7 +28,7 @@ __global__ __launch_bounds__(kTile) void iov_len_kernel(IovArgs a) {
     uint64_t len = 0, hl = 0;
     if (r < a.n) {
         const onc_msg d = a.msgs[r];
-        const RecPlan p = plan_record(d, a.unix);
+        const RecPlan p = plan_record(d, a.unix, a.bounds);
         len = p.len;
         hl = p.len ? 4ull * meta_hw(p.meta) : 0;
         a.status[r] = p.status;
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(64 * kIovWaves) void iov_emit_kernel(IovArgs a) {
     uint64_t len = 0, hl = 0;
     if (lane < nrec) {
         d = a.msgs[r0 + lane];
-        const RecPlan p = plan_record(d, a.unix);
+        const RecPlan p = plan_record(d, a.unix, a.bounds);
         len = p.len;
         hl = p.len ? 4ull * meta_hw(p.meta) : 0;
     }

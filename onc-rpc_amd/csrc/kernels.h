@@ -16,8 +16,10 @@ struct EncArgs {
     const onc_unix_params* unix;
     const uint8_t* auth_arena;
     const uint8_t* payload_arena;
-    uint8_t* out;
-    uint64_t out_cap;
+    Bounds bounds;          // arena sizes (onc_batch)
+    uint8_t* out;           // 16-byte aligned base of the output chunks
+    uint64_t origin;        // byte offset of the caller's `out` from `out` here (0..15)
+    uint64_t out_cap;       // origin + the caller's capacity
     uint64_t* rec_off;      // n + 1
     int32_t* status;        // n
     uint32_t* rec_len;      // n, optional
@@ -38,6 +40,7 @@ struct IovArgs {
     const onc_unix_params* unix;
     const uint8_t* auth_arena;
     const uint8_t* payload_arena;
+    Bounds bounds;
     uint8_t* hdr_out;
     uint64_t hdr_cap;
     onc_iov_rec* iov;

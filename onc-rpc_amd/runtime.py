@@ -18,11 +18,12 @@ _LIB = None
 LIB_PATH = os.environ.get("ONC_RPC_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libonc_rpc_amd.so")
 
 K_NAMES = ["enc_len_kernel", "scan_tiles_kernel", "enc_emit_kernel", "decode_kernel",
-           "len_tiles_kernel", "len_apply_kernel", "enc_fixup_kernel", "iov_len_kernel", "iov_emit_kernel",
+           "len_tiles_kernel", "len_apply_kernel", "iov_len_kernel", "iov_emit_kernel",
            "frame_chunks_kernel", "frame_write_kernel", "frame_verify_kernel", "frame_walk_kernel",
            "frame_counts_kernel", "frame_guess_kernel"]
-(K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY, K_ENC_FIXUP, K_IOV_LEN,
- K_IOV_EMIT, K_FRAME, K_FRAME_WRITE, K_FRAME_VERIFY, K_FRAME_WALK, K_FRAME_COUNTS, K_FRAME_GUESS) = range(15)
+(K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY, K_IOV_LEN,
+ K_IOV_EMIT, K_FRAME, K_FRAME_WRITE, K_FRAME_VERIFY, K_FRAME_WALK, K_FRAME_COUNTS, K_FRAME_GUESS) = range(14)
+ABI_VERSION = 2
 K_COUNT = len(K_NAMES)
 
 # every symbol include/onc_rpc.h declares
@@ -37,7 +38,8 @@ EXPORTED = [
 
 class OncBatch(C.Structure):
     _fields_ = [("n", C.c_uint64), ("msgs", C.c_void_p), ("unix_params", C.c_void_p),
-                ("auth_arena", C.c_void_p), ("payload_arena", C.c_void_p)]
+                ("auth_arena", C.c_void_p), ("payload_arena", C.c_void_p),
+                ("unix_count", C.c_uint64), ("auth_len", C.c_uint64), ("payload_len", C.c_uint64)]
 
 
 class OncDecoded(C.Structure):
@@ -114,14 +116,20 @@ def to_device(arr, device):
 
 
 class DeviceBatch:
-    """Descriptor batch resident in HBM (torch uint8 tensors)."""
+    """Descriptor batch resident in HBM (torch uint8 tensors). The arena
+    sizes handed to the codec (onc_batch bounds) are the tensors' sizes
+    unless given."""
 
-    def __init__(self, n, msgs, unix, auth_arena, payload_arena):
+    def __init__(self, n, msgs, unix, auth_arena, payload_arena, unix_count=None, auth_len=None,
+                 payload_len=None):
         self.n = n
         self.msgs = msgs
         self.unix = unix
         self.auth_arena = auth_arena
         self.payload_arena = payload_arena
+        self.unix_count = unix.numel() // 96 if unix_count is None else unix_count
+        self.auth_len = auth_arena.numel() if auth_len is None else auth_len
+        self.payload_len = payload_arena.numel() if payload_len is None else payload_len
 
     @classmethod
     def from_host(cls, hb: L.HostBatch, device="cuda"):
@@ -130,7 +138,8 @@ class DeviceBatch:
 
     def c_struct(self):
         return OncBatch(self.n, self.msgs.data_ptr(), self.unix.data_ptr(),
-                        self.auth_arena.data_ptr(), self.payload_arena.data_ptr())
+                        self.auth_arena.data_ptr(), self.payload_arena.data_ptr(),
+                        self.unix_count, self.auth_len, self.payload_len)
 
 
 class Codec:

@@ -232,3 +232,42 @@ def corrupt(wire: np.ndarray, rec_off: np.ndarray, frac=0.05, seed=7):
             r[j:j + 4] = int(rng.integers(0, 300)).to_bytes(4, "big")
         recs[i] = r
     return L.records_from_wire([bytes(r) for r in recs])
+
+
+def call_none_device(lo, hi, payload_len=256, seed=1, device="cuda"):
+    """configs[1]/[4] records [lo, hi) generated directly in HBM (torch on the
+    device; a 64M-record batch is 16.4 GB of payload, too much to build in
+    host numpy and copy): the descriptors of call_none (xid = record index,
+    prog 100003, vers 4, proc 1, AuthNone(None) x2, payload_len bytes at
+    payload_off = (i - lo) * payload_len) and a device-RNG payload arena
+    (torch.Generator seeded with (seed, lo), so every shard is reproducible
+    on its own). Returns (runtime.DeviceBatch, generator seed)."""
+    import torch
+
+    from . import runtime as R
+    n = hi - lo
+    m = torch.zeros((max(n, 1), 16), dtype=torch.int32, device=device)
+    if n:
+        m[:n, 0] = (torch.arange(lo, hi, dtype=torch.int64, device=device) & 0xFFFFFFFF).to(torch.int32)
+        m[:n, 2], m[:n, 3], m[:n, 4], m[:n, 5] = 100003, 4, 1, payload_len
+        m.view(torch.int64)[:n, 3] = torch.arange(n, dtype=torch.int64, device=device) * payload_len
+    gseed = (int(seed) * 1_000_003 + int(lo)) & 0x7FFFFFFFFFFFFFFF
+    g = torch.Generator(device=device)
+    g.manual_seed(gseed)
+    payload = torch.randint(0, 256, (n * payload_len + 16,), dtype=torch.uint8, device=device, generator=g)
+    msgs = m.view(torch.uint8).reshape(-1)
+    unix = torch.zeros(96, dtype=torch.uint8, device=device)
+    auth = torch.zeros(16, dtype=torch.uint8, device=device)
+    return R.DeviceBatch(n, msgs, unix, auth, payload), gseed
+
+
+def host_window(db, lo, hi):
+    """Records [lo, hi) of a call_none_device batch as a host HostBatch
+    (descriptors + their payload bytes, offsets rebased) for an oracle check."""
+    import numpy as np
+    msgs = db.msgs.view(-1, 64)[lo:hi].cpu().numpy().copy().view(L.MSG_DTYPE).reshape(-1)
+    p0 = int(msgs["payload_off"][0]) if hi > lo else 0
+    p1 = int((msgs["payload_off"].astype(np.int64) + msgs["payload_len"]).max()) if hi > lo else 0
+    pay = db.payload_arena[p0:p1 + 16].cpu().numpy().copy()
+    msgs["payload_off"] -= np.uint64(p0)
+    return L.HostBatch(msgs, np.zeros(1, L.UNIX_DTYPE), np.zeros(16, np.uint8), pay)

@@ -14,6 +14,18 @@ LIB_PATH = os.path.join(HERE, "liboncoracle.so")
 _LIB = None
 
 
+def use_library(path):
+    """Swap in another build of the same oracle source (bench.py's CPU
+    baseline compiles oracle/onc_oracle.c with -O3 -march=native on the host
+    it runs on). Returns the previous library path."""
+    global _LIB, LIB_PATH
+    prev = LIB_PATH
+    LIB_PATH = path
+    _LIB = None
+    load()
+    return prev
+
+
 def load():
     global _LIB
     if _LIB is not None:

@@ -33,7 +33,7 @@ def test_library_exports_every_header_symbol():
     import onc_rpc_amd.runtime as R
     assert sorted(R.EXPORTED) == funcs
     lib.onc_abi_version.restype = C.c_int
-    assert lib.onc_abi_version() == 1
+    assert lib.onc_abi_version() == 2
     lib.onc_status_str.restype = C.c_char_p
     assert lib.onc_status_str(1) == b"incomplete rpc message"
 
@@ -164,3 +164,26 @@ def test_expected_message_len_matches_oracle(oracle, golden):
             assert st == want, b.hex()
             if st == 0:
                 assert got == w.value
+
+
+def test_batch_struct_matches_ctypes():
+    """onc_batch (ABI v2: arena sizes) as the ctypes binding lays it out."""
+    import onc_rpc_amd.runtime as R
+    prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "onc_rpc.h"
+int main(void){
+ printf("%zu %zu %zu %zu %zu\n", sizeof(onc_batch), offsetof(onc_batch,payload_arena),
+        offsetof(onc_batch,unix_count), offsetof(onc_batch,auth_len), offsetof(onc_batch,payload_len));
+ return 0;}
+'''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(prog)
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+        vals = [int(x) for x in subprocess.check_output([exe]).split()]
+    B = R.OncBatch
+    assert vals == [C.sizeof(B), B.payload_arena.offset, B.unix_count.offset, B.auth_len.offset,
+                    B.payload_len.offset]
