@@ -448,21 +448,38 @@ class Timing:
     kernel's launches bracketed by HIP events on the codec's stream; and an
     event-free pass of the same K steps."""
 
-    def __init__(self, torch, R, codec, step, steps, warmup, barrier):
+    def __init__(self, torch, R, codec, step, steps, warmup, barrier, codecs=None, drain=None):
+        codecs = codecs or [codec]
+        drain = drain or (lambda: None)
+
+        def stats():
+            tot = {}
+            for c in codecs:
+                for k, (ms, cnt) in c.kernel_stats().items():
+                    a, b = tot.get(k, (0.0, 0))
+                    tot[k] = (a + ms, b + cnt)
+            return tot
+
+        def timing(on, kernels=None):
+            for c in codecs:
+                c.enable_timing(on, kernels=kernels)
+
         for _ in range(warmup):
             step()
         torch.cuda.synchronize()
-        codec.reset_stats()
-        codec.enable_timing(True)
+        for c in codecs:
+            c.reset_stats()
+        timing(True)
         for _ in range(steps):
             step()
         torch.cuda.synchronize()
-        codec.enable_timing(False)
-        self.breakdown = codec.kernel_stats()
+        timing(False)
+        self.breakdown = stats()
         self.dom_id = max(range(R.K_COUNT),
                           key=lambda k: self.breakdown[R.K_NAMES[k]][0] / max(1, self.breakdown[R.K_NAMES[k]][1]))
-        codec.reset_stats()
-        codec.enable_timing(True, kernels=[self.dom_id])
+        for c in codecs:
+            c.reset_stats()
+        timing(True, kernels=[self.dom_id])
         barrier()
         torch.cuda.synchronize()
         ev0 = torch.cuda.Event(enable_timing=True)
@@ -471,19 +488,21 @@ class Timing:
         ev0.record()
         for _ in range(steps):
             step()
+        drain()
         ev1.record()
         torch.cuda.synchronize()
         barrier()
         self.wall_s = time.perf_counter() - t_wall0
-        codec.enable_timing(False)
+        timing(False)
         self.ms = ev0.elapsed_time(ev1)
-        self.kstats = codec.kernel_stats()
+        self.kstats = stats()
         torch.cuda.synchronize()
         ev2 = torch.cuda.Event(enable_timing=True)
         ev3 = torch.cuda.Event(enable_timing=True)
         ev2.record()
         for _ in range(steps):
             step()
+        drain()
         ev3.record()
         torch.cuda.synchronize()
         self.ms_clean = ev2.elapsed_time(ev3)

@@ -23,6 +23,7 @@ struct onc_codec {
     uint64_t frame_chunks = 0;
     uint64_t frame_chunk = onc::kFrameChunkDefault;   // ONC_RPC_FRAME_CHUNK at create (bytes, >= 64)
     bool force_scan = false;   // ONC_RPC_FORCE_SCAN=1 at create: always launch the block scan (tests)
+    uint32_t variant = 0;      // ONC_RPC_VARIANT at create: kernel variant bits (A/B measurements)
     uint32_t timing = 0;   // bitmask of ONC_K_* ids whose launches are bracketed
     struct Pending {
         int kernel;
@@ -128,6 +129,8 @@ int onc_codec_create(onc_codec** out, int device, void* hip_stream) {
     c->stream = static_cast<hipStream_t>(hip_stream);
     const char* fs = getenv("ONC_RPC_FORCE_SCAN");
     c->force_scan = fs && fs[0] == '1';
+    const char* vv = getenv("ONC_RPC_VARIANT");
+    if (vv) c->variant = uint32_t(strtoul(vv, nullptr, 0));
     const char* fc = getenv("ONC_RPC_FRAME_CHUNK");
     if (fc) {
         const unsigned long long v = strtoull(fc, nullptr, 10);
@@ -330,6 +333,7 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
     // itself and the scan launch is skipped.
     const uint64_t nblk = onc::num_len_blocks(batch->n);
     a.fused_base = nblk <= onc::kFusedBlocks && !c->force_scan;
+    a.variant = c->variant;
     rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
     if (!a.fused_base) {
@@ -479,6 +483,7 @@ int onc_decode(onc_codec* c, const uint8_t* wire, const uint64_t* rec_off, uint6
     a.wire = wire;
     a.rec_off = rec_off;
     a.out = *out;
+    a.variant = c->variant;
     return run(c, ONC_K_DEC_PARSE, "decode", [&] { return onc::launch_decode(a, mode, c->stream); });
 }
 

@@ -27,6 +27,7 @@ struct EncArgs {
     uint64_t* block_sum;    // enc_len workgroups (kLenRecs records): byte totals
     uint64_t* block_base;   // exclusive scan of block_sum (unused when fused_base)
     uint32_t fused_base;    // enc_emit sums block_sum itself (<= kFusedBlocks workgroups; no scan launch)
+    uint32_t variant;       // ONC_RPC_VARIANT bits (A/B experiments)
 };
 
 // Batches of at most this many enc_len workgroups (1M records) skip the
@@ -87,6 +88,7 @@ struct DecArgs {
     const uint8_t* wire;
     const uint64_t* rec_off;
     onc_decoded out;
+    uint32_t variant;       // ONC_RPC_VARIANT bits (A/B experiments)
 };
 
 // encode.hip

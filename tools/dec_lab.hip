@@ -42,6 +42,48 @@ __global__ __launch_bounds__(256) void l_read(DecArgs a) {
     a.out.status[i] = int32_t(x == 0x12345678u);
 }
 
+// read-only, R records per lane (records i0 + t + 256 j of a 256 R block),
+// every window load of the lane issued before any is used
+template <int NCH, int R>
+__global__ __launch_bounds__(256) void l_read_r(DecArgs a) {
+    const uint64_t i0 = uint64_t(blockIdx.x) * 256 * R;
+    u32x4 v[R][NCH];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint64_t i = min(i0 + threadIdx.x + 256 * r, a.n - 1);
+        const uintptr_t win = (reinterpret_cast<uintptr_t>(a.wire) + a.rec_off[i]) & ~uintptr_t(15);
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) v[r][j] = gload<u32x4>(win + 16 * j);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint64_t i = i0 + threadIdx.x + 256 * r;
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) x ^= v[r][j].x ^ v[r][j].y ^ v[r][j].z ^ v[r][j].w;
+        if (i < a.n) a.out.status[i] = int32_t(x == 0x12345678u);
+    }
+}
+
+// coalesced sweep: the workgroup reads its 256 records' whole byte range
+// (headers and payloads) with 16 B per lane per step, XOR-folded
+__global__ __launch_bounds__(256) void l_sweep(DecArgs a) {
+    const uint64_t i0 = uint64_t(blockIdx.x) * 256;
+    const uint64_t i1 = min(i0 + 256, a.n);
+    const uintptr_t w = reinterpret_cast<uintptr_t>(a.wire);
+    const uintptr_t lo = (w + a.rec_off[i0]) & ~uintptr_t(15), hi = w + a.rec_off[i1];
+    uint32_t x = 0;
+    for (uintptr_t p = lo + 16 * threadIdx.x; p < hi; p += 16 * 256 * 4) {
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = gload<u32x4>(min(p + 16 * 256 * k, (hi - 1) & ~uintptr_t(15)));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    const uint64_t i = i0 + threadIdx.x;
+    if (i < a.n) a.out.status[i] = int32_t(x == 0x12345678u);
+}
+
 // read window + write descriptors (LDS staged) + status/aux
 template <int NCH>
 __global__ __launch_bounds__(256) void l_rw(DecArgs a) {
@@ -132,6 +174,12 @@ int main(int argc, char** argv) {
         {"read 4 + write", [&] { hipLaunchKernelGGL(l_rw<4>, dim3(grid), dim3(256), 0, 0, a); }, {}},
         {"read 3 + write", [&] { hipLaunchKernelGGL(l_rw<3>, dim3(grid), dim3(256), 0, 0, a); }, {}},
         {"write only", [&] { hipLaunchKernelGGL(l_write, dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"read 4, 2 rec/lane", [&] { hipLaunchKernelGGL((l_read_r<4, 2>), dim3((grid + 1) / 2), dim3(256), 0, 0, a); }, {}},
+        {"read 4, 4 rec/lane", [&] { hipLaunchKernelGGL((l_read_r<4, 4>), dim3((grid + 3) / 4), dim3(256), 0, 0, a); }, {}},
+        {"read 2, 1 rec/lane", [&] { hipLaunchKernelGGL((l_read_r<2, 1>), dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"read 1, 1 rec/lane", [&] { hipLaunchKernelGGL((l_read_r<1, 1>), dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"sweep whole range", [&] { hipLaunchKernelGGL(l_sweep, dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"read 1, 4 rec/lane", [&] { hipLaunchKernelGGL((l_read_r<1, 4>), dim3((grid + 3) / 4), dim3(256), 0, 0, a); }, {}},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
