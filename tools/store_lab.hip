@@ -1,0 +1,121 @@
+// store_lab.hip — cache-policy bits of streaming stores on gfx950 (dev tool).
+//
+// A 256 MiB copy (16 B per lane, two loads in flight) whose stores carry a
+// given policy (none / nt / sc1 / nt sc1 / sc0 sc1 / nt sc0 sc1), followed by
+// a read of another 320 MiB buffer: the second kernel pays for whatever the
+// first left dirty in L2 / the Infinity Cache, so the pair shows the policy's
+// cost to the next kernel too (enc_emit -> decode in the product step).
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/store_lab.hip -o tools/store_lab
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int P>
+__device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
+    if constexpr (P == 0) *p = v;
+    else if constexpr (P == 1) __builtin_nontemporal_store(v, p);
+    else if constexpr (P == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (P == 3) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (P == 4) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (P == 5) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off sc0" ::"v"(p), "v"(v) : "memory");
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void copy_k(const u32x4* __restrict__ in, u32x4* __restrict__ out, uint64_t n16) {
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n16; i += 2 * stride) {
+        const u32x4 a = in[i];
+        const u32x4 b = i + stride < n16 ? in[i + stride] : u32x4{0, 0, 0, 0};
+        st16<P>(out + i, a);
+        if (i + stride < n16) st16<P>(out + i + stride, b);
+    }
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void write_k(u32x4* __restrict__ out, uint64_t n16) {
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n16; i += stride)
+        st16<P>(out + i, u32x4{uint32_t(i), 1, 2, 3});
+}
+
+__global__ __launch_bounds__(256) void read_k(const u32x4* __restrict__ in, uint64_t n16, uint32_t* sink) {
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    uint32_t x = 0;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n16; i += stride) {
+        const u32x4 v = in[i];
+        x ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (x == 0x9e3779b9u) sink[0] = x;
+}
+
+int main() {
+    const size_t nb = size_t(256) << 20, ob = size_t(320) << 20;
+    void *src, *dst, *other;
+    uint32_t* sink;
+    CK(hipMalloc(&src, nb));
+    CK(hipMalloc(&dst, nb));
+    CK(hipMalloc(&other, ob));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMemset(src, 1, nb));
+    CK(hipMemset(other, 2, ob));
+    const uint64_t n16 = nb / 16, o16 = ob / 16;
+    const char* names[7] = {"plain", "nt", "sc1", "sc1 nt", "sc0 sc1", "sc0 sc1 nt", "sc0"};
+    typedef void (*CopyF)(const u32x4*, u32x4*, uint64_t);
+    typedef void (*WriteF)(u32x4*, uint64_t);
+    CopyF cf[7] = {copy_k<0>, copy_k<1>, copy_k<2>, copy_k<3>, copy_k<4>, copy_k<5>, copy_k<6>};
+    WriteF wf[7] = {write_k<0>, write_k<1>, write_k<2>, write_k<3>, write_k<4>, write_k<5>, write_k<6>};
+    std::vector<float> t[7][4];
+    hipEvent_t e[3];
+    for (auto& x : e) CK(hipEventCreate(&x));
+    for (int rep = 0; rep < 12; ++rep) {
+        for (int p = 0; p < 7; ++p) {
+            for (int mode = 0; mode < 2; ++mode) {
+                CK(hipMemset(other, rep, ob));   // a third buffer's traffic in between: no carry-over
+                CK(hipDeviceSynchronize());
+                CK(hipEventRecord(e[0], 0));
+                if (mode == 0)
+                    hipLaunchKernelGGL(cf[p], dim3(4096), dim3(256), 0, 0, (const u32x4*)src, (u32x4*)dst, n16);
+                else
+                    hipLaunchKernelGGL(wf[p], dim3(8192), dim3(256), 0, 0, (u32x4*)dst, n16);
+                CK(hipEventRecord(e[1], 0));
+                hipLaunchKernelGGL(read_k, dim3(8192), dim3(256), 0, 0, (const u32x4*)other, o16, sink);
+                CK(hipEventRecord(e[2], 0));
+                CK(hipEventSynchronize(e[2]));
+                float a, b;
+                CK(hipEventElapsedTime(&a, e[0], e[1]));
+                CK(hipEventElapsedTime(&b, e[1], e[2]));
+                if (rep >= 2) {
+                    t[p][2 * mode].push_back(a * 1000.f);
+                    t[p][2 * mode + 1].push_back(b * 1000.f);
+                }
+            }
+        }
+    }
+    printf("%-12s %12s %12s %12s | %12s %12s %12s\n", "store policy", "copy256", "next rd320", "sum", "write256",
+           "next rd320", "sum");
+    for (int p = 0; p < 7; ++p) {
+        float m[4];
+        for (int k = 0; k < 4; ++k) {
+            std::sort(t[p][k].begin(), t[p][k].end());
+            m[k] = t[p][k][t[p][k].size() / 2];
+        }
+        printf("%-12s %12.1f %12.1f %12.1f | %12.1f %12.1f %12.1f\n", names[p], m[0], m[1], m[0] + m[1], m[2], m[3],
+               m[2] + m[3]);
+    }
+    return 0;
+}
