@@ -136,6 +136,16 @@ __device__ __forceinline__ uint64_t tile_reduce(const TileLoads<kFused>& t, uint
 
 constexpr int kFastWaves = 4;                 // wave tiles per enc_emit workgroup
 
+// Phase timestamps of a tile (lab builds with -DONC_EMIT_PROF only):
+// 0 start, 1 placement known, 2 plan + scan done, 3 span staged in LDS,
+// 4 span streamed, 5 tile done (s_memrealtime, 100 MHz).
+#ifdef ONC_EMIT_PROF
+#define ONC_PROF(k) \
+    do { if (a.prof && (threadIdx.x & 63) == 0) a.prof[8 * tile + (k)] = wall_clock64(); } while (0)
+#else
+#define ONC_PROF(k) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // enc_emit (chunk image): every load of a step in flight.
 // ---------------------------------------------------------------------------
@@ -387,6 +397,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
 
     // Prologue: the tile-placement loads and this lane's descriptor issued
     // together, one memory round trip before the planning starts.
+    ONC_PROF(0);
     TileLoads<kFused> tl = tile_loads<kFused>(a, tile);
     MsgRegs mr = issue_msg(a.msgs + r0 + min(lane, nrec - 1));
     if constexpr (kFused) {
@@ -402,6 +413,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     // output coordinates: byte 0 = the 16-aligned chunk base below the
     // caller's `out`, which sits at `origin` (any writer position)
     const uint64_t T0 = a.origin + tile_reduce<kFused>(tl, tile);
+    ONC_PROF(1);
     uint64_t len = 0, poff = 0;
     uint32_t hw = 0;
     bool word_aligned = true;
@@ -437,6 +449,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     const uint64_t plen = en - pst;
 
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.msgs);   // >= 64 valid bytes
+    ONC_PROF(2);
     int lo_rec = 0;
     while (lo_rec < nrec) {
         // span: records [lo_rec, hi_rec) whose non-pure chunks (+1 for a
@@ -496,6 +509,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         }
         if (lane == 0) T.ent[ns] = make_int4(0x7FFFFFFF, 0, 0, 0);
         wave_lds_sync();
+        if (lo_rec == 0) ONC_PROF(3);
 
         const uint64_t E = min(S1, a.out_cap);
         lo_rec = hi_rec;
@@ -503,7 +517,9 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         const int32_t NCe = int32_t(((E + 15) >> 4) - C0);
         if (byte_mode) stream_span<1, kNT, true>(a, T, gsh, B0, S0, E, NCe, dummy);
         else stream_span<kU, kNT, false>(a, T, gsh, B0, S0, E, NCe, dummy);
+        if (lo_rec == hi_rec && hi_rec == nrec) ONC_PROF(4);
     }
+    ONC_PROF(5);
 }
 
 // kNT: bit 0 = nontemporal payload loads, bit 1 = nontemporal stores (a

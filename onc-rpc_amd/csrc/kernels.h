@@ -28,6 +28,9 @@ struct EncArgs {
     uint64_t* block_base;   // exclusive scan of block_sum (unused when fused_base)
     uint32_t fused_base;    // enc_emit sums block_sum itself (<= kFusedBlocks workgroups; no scan launch)
     uint32_t variant;       // ONC_RPC_VARIANT bits (A/B experiments)
+#ifdef ONC_EMIT_PROF
+    uint64_t* prof;         // lab builds only (tools/emit_prof.hip): per-tile phase timestamps
+#endif
 };
 
 // Batches of at most this many enc_len workgroups (1M records) skip the

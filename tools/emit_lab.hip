@@ -292,6 +292,7 @@ int main(int argc, char** argv) {
     a.unix = d_unix;
     a.auth_arena = d_auth;
     a.payload_arena = d_pay;
+    a.bounds = Bounds{1, 64, pay.size()};
     a.out = d_out;
     a.out_cap = n * W;
     a.rec_off = d_off;

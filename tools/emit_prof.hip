@@ -1,0 +1,157 @@
+// emit_prof.hip — where an enc_emit wave's time goes (dev tool).
+//
+// Builds the product encode.hip with -DONC_EMIT_PROF: every tile records
+// s_memrealtime (100 MHz) at its phase boundaries (start, placement known,
+// plan + scan, span staged in LDS, span streamed, done). Runs enc_len +
+// enc_emit on a configs[1] batch (or configs[3] with argv[2] = "c3") and
+// prints the mean / median duration of every phase per tile, the mean tile
+// lifetime and the mean number of tiles in flight.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -DONC_EMIT_PROF tools/emit_prof.hip -o tools/emit_prof
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../onc-rpc_amd/csrc/encode.hip"
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+using namespace onc;
+
+int main(int argc, char** argv) {
+    const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1000000;
+    const bool c3 = argc > 2 && std::string(argv[2]) == "c3";
+    const uint32_t P = c3 ? 1024 : 256;
+    std::vector<onc_msg> msgs(n);
+    std::vector<onc_unix_params> unix(c3 ? n : 1);
+    const uint32_t gids[16] = {501, 12, 20, 61, 79, 80, 81, 98, 701, 33, 100, 204, 250, 395, 398, 399};
+    for (uint64_t i = 0; i < n; ++i) {
+        onc_msg& m = msgs[i];
+        memset(&m, 0, sizeof(m));
+        m.xid = uint32_t(i);
+        m.msg_type = ONC_MSG_CALL;
+        m.u.call.program = 100003;
+        m.u.call.program_version = 4;
+        m.u.call.procedure = 1;
+        m.payload_len = P;
+        m.payload_off = i * P;
+        m.verf.kind_len = ONC_AUTH_PACK(ONC_KIND_NONE, 0);
+        if (c3) {
+            m.cred.id = ONC_AUTH_UNIX;
+            m.cred.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
+            m.cred.ref = i;
+            onc_unix_params& u = unix[i];
+            memset(&u, 0, sizeof(u));
+            u.stamp = uint32_t(i);
+            u.uid = 501;
+            u.gid = 20;
+            u.ngids = 16;
+            memcpy(u.gids, gids, sizeof(gids));
+        }
+    }
+    std::vector<uint8_t> pay(n * P + 16);
+    std::mt19937_64 rng(1);
+    for (auto& b : pay) b = uint8_t(rng());
+    const uint64_t W = c3 ? 128 + P : 44 + P;
+
+    onc_msg* d_msgs;
+    onc_unix_params* d_unix;
+    uint8_t *d_pay, *d_out, *d_auth;
+    uint64_t *d_off, *d_scr, *d_prof;
+    int32_t* d_st;
+    const uint64_t tiles = num_emit_tiles(n);
+    CK(hipMalloc(&d_msgs, n * sizeof(onc_msg)));
+    CK(hipMalloc(&d_unix, unix.size() * sizeof(onc_unix_params)));
+    CK(hipMalloc(&d_pay, pay.size()));
+    CK(hipMalloc(&d_out, n * W + 64));
+    CK(hipMalloc(&d_auth, 64));
+    CK(hipMalloc(&d_off, (n + 1) * 8));
+    CK(hipMalloc(&d_scr, (3 * tiles + 2 * (tiles / 4 + 1) + 16) * 8));
+    CK(hipMalloc(&d_st, n * 4));
+    CK(hipMalloc(&d_prof, tiles * 8 * 8));
+    CK(hipMemcpy(d_msgs, msgs.data(), n * sizeof(onc_msg), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_unix, unix.data(), unix.size() * sizeof(onc_unix_params), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_pay, pay.data(), pay.size(), hipMemcpyHostToDevice));
+
+    EncArgs a{};
+    a.n = n;
+    a.msgs = d_msgs;
+    a.unix = d_unix;
+    a.auth_arena = d_auth;
+    a.payload_arena = d_pay;
+    a.bounds = Bounds{unix.size(), 64, pay.size()};
+    a.out = d_out;
+    a.out_cap = n * W;
+    a.rec_off = d_off;
+    a.status = d_st;
+    a.tile_sum = d_scr;
+    a.block_sum = d_scr + 3 * tiles;
+    a.block_base = d_scr + 3 * tiles + tiles / 4 + 1;
+    a.fused_base = num_len_blocks(n) <= kFusedBlocks;
+    if (!a.fused_base) {
+        fprintf(stderr, "n too large for the fused placement (lab keeps to <= 1M records)\n");
+        return 1;
+    }
+    a.prof = nullptr;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float best = 1e9f;
+    for (int rep = 0; rep < 12; ++rep) {
+        CK(launch_enc_len(a, 0));
+        a.prof = rep >= 6 ? d_prof : nullptr;
+        CK(hipEventRecord(e0, 0));
+        CK(launch_enc_emit(a, 0));
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (rep >= 6) best = std::min(best, ms);
+        if (rep < 6) printf("unprofiled enc_emit %.1f us\n", ms * 1000);
+    }
+    std::vector<uint64_t> prof(tiles * 8);
+    CK(hipMemcpy(prof.data(), d_prof, prof.size() * 8, hipMemcpyDeviceToHost));
+    uint64_t t_min = ~0ull, t_max = 0;
+    const char* names[5] = {"prologue loads (0->1)", "plan + scan (1->2)", "header build + map (2->3)",
+                            "stream (3->4)", "tail (4->5)"};
+    std::vector<double> d[5], life;
+    for (uint64_t t = 0; t < tiles; ++t) {
+        const uint64_t* p = &prof[8 * t];
+        t_min = std::min(t_min, p[0]);
+        t_max = std::max(t_max, p[5]);
+        for (int k = 0; k < 5; ++k) d[k].push_back(double(p[k + 1] - p[k]) * 10.0 / 1000.0);   // us
+        life.push_back(double(p[5] - p[0]) * 10.0 / 1000.0);
+    }
+    double sum_life = 0;
+    for (double x : life) sum_life += x;
+    const double span_us = double(t_max - t_min) * 10.0 / 1000.0;
+    printf("%s: %llu records, %llu tiles; profiled enc_emit %.1f us (events); first tile start -> last tile end %.1f us\n",
+           c3 ? "configs[3]" : "configs[1]", (unsigned long long)n, (unsigned long long)tiles, best * 1000, span_us);
+    printf("mean tile lifetime %.2f us; mean tiles in flight %.0f\n", sum_life / tiles, sum_life / span_us);
+    for (int k = 0; k < 5; ++k) {
+        std::sort(d[k].begin(), d[k].end());
+        double s = 0;
+        for (double x : d[k]) s += x;
+        printf("  %-28s mean %6.2f us  median %6.2f  p90 %6.2f\n", names[k], s / tiles, d[k][tiles / 2],
+               d[k][tiles * 9 / 10]);
+    }
+    // time profile: tiles started per 5% of the kernel
+    printf("tiles started per 10%% of the span:");
+    std::vector<int> hist(10);
+    for (uint64_t t = 0; t < tiles; ++t) hist[std::min<uint64_t>(9, (prof[8 * t] - t_min) * 10 / (t_max - t_min + 1))]++;
+    for (int h : hist) printf(" %d", h);
+    printf("\n");
+    return 0;
+}
