@@ -672,6 +672,7 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
     n = hi - lo
     if wl == "c1":
         hb = S.call_none(n, 256, seed=1 + rank, first_xid=lo)
+
         desc = "configs[1]: Call(prog 100003, vers 4, proc 1, AuthNone(None) x2) + 256 B payload, encode -> decode"
     elif wl == "c2":
         hb = S.mixed(n, seed=2 + rank)
