@@ -500,6 +500,14 @@ int onc_scan_lengths(onc_codec* c, const uint32_t* rec_len, uint64_t n, uint64_t
     if (rc != ONC_RC_OK) return rc;
     uint64_t* tile_sum = c->scratch;
     uint64_t* tile_base = c->scratch + c->scratch_tiles;
+    if (onc::scan_lengths_fused_ok(n) && !c->force_scan) {
+        // two launches: 4096-record block totals, then every block sums the
+        // totals before it and scans its own lengths
+        rc = run(c, ONC_K_LEN_TILES, "lenblk", [&] { return onc::launch_lenblk(rec_len, n, tile_sum, c->stream); });
+        if (rc != ONC_RC_OK) return rc;
+        return run(c, ONC_K_LEN_APPLY, "lenoff",
+                   [&] { return onc::launch_lenoff(rec_len, n, tile_sum, base, rec_off, c->stream); });
+    }
     rc = run(c, ONC_K_LEN_TILES, "len_tiles", [&] { return onc::launch_len_tiles(rec_len, n, tile_sum, c->stream); });
     if (rc != ONC_RC_OK) return rc;
     rc = run(c, ONC_K_SCAN_TILES, "scan_tiles",

@@ -113,6 +113,10 @@ hipError_t launch_scan_tiles(const uint64_t* in, uint64_t* out_excl, uint64_t co
 hipError_t launch_len_tiles(const uint32_t* len, uint64_t n, uint64_t* tile_sum, hipStream_t s);
 hipError_t launch_len_apply(const uint32_t* len, uint64_t n, const uint64_t* tile_base, uint64_t* rec_off,
                             hipStream_t s);
+bool scan_lengths_fused_ok(uint64_t n);
+hipError_t launch_lenblk(const uint32_t* len, uint64_t n, uint64_t* blk_sum, hipStream_t s);
+hipError_t launch_lenoff(const uint32_t* len, uint64_t n, const uint64_t* blk_sum, uint64_t base, uint64_t* rec_off,
+                         hipStream_t s);
 // decode.hip
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s);
 

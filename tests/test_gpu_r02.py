@@ -307,3 +307,38 @@ def test_two_ranks_hip_codec_concatenate(codec, R, oracle, tmp_path):
             for slot, f in ((2 * i, "cred"), (2 * i + 1, "verf")):
                 if (int(om[f + "_kind_len"][i]) >> 24) == L.KIND_UNIX:
                     assert cu[slot].tobytes() == ou[slot].tobytes()
+
+
+@pytest.mark.parametrize("force", [False, True])
+def test_scan_lengths_sizes_and_alignment(R, force):
+    """onc_scan_lengths: the two-launch path (lenblk -> lenoff, up to 8M
+    records) and the three-launch path (ONC_RPC_FORCE_SCAN=1, or beyond 8M)
+    at block boundaries, with misaligned length / offset pointers (slices):
+    rec_off = base + exclusive prefix sum, rec_off[n] = base + total."""
+    import torch
+    old = os.environ.get("ONC_RPC_FORCE_SCAN")
+    os.environ["ONC_RPC_FORCE_SCAN"] = "1" if force else "0"
+    try:
+        c = R.Codec(0)
+    finally:
+        if old is None:
+            del os.environ["ONC_RPC_FORCE_SCAN"]
+        else:
+            os.environ["ONC_RPC_FORCE_SCAN"] = old
+    rng = np.random.default_rng(11)
+    sizes = [1, 15, 16, 17, 4095, 4096, 4097, 8191, 65536 + 3, 2048 * 4096, 2048 * 4096 + 1]
+    for n in sizes:
+        lens = rng.integers(0, 1 << 31, n, dtype=np.uint64).astype(np.uint32) if n < 100 else \
+            rng.integers(0, 5000, n).astype(np.uint32)
+        for lshift, oshift in ((0, 0), (1, 1), (3, 2)):
+            if n > 100000 and (lshift, oshift) != (0, 0):
+                continue
+            d = torch.zeros(n + lshift, dtype=torch.int32, device="cuda")
+            d[lshift:] = torch.from_numpy(lens.view(np.int32).copy()).cuda()
+            off = torch.zeros(n + 1 + oshift, dtype=torch.int64, device="cuda")
+            c.scan_lengths(d[lshift:], n, 987654321, off[oshift:])
+            c.sync()
+            want = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))]) + np.uint64(987654321)
+            got = off[oshift:].cpu().numpy().view(np.uint64)
+            assert np.array_equal(got, want), (n, lshift, oshift, np.nonzero(got != want)[0][:5])
+    c.close()
