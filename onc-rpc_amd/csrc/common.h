@@ -413,17 +413,44 @@ __device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len,
 }
 
 // ---------------------------------------------------------------------------
-// Block-wide exclusive scan of u64 over 256 threads (4 waves)
+// Cross-lane primitives on DPP / readlane (no LDS round trip)
 // ---------------------------------------------------------------------------
+// DPP controls (GFX9 encoding): row_shr:n = 0x110 + n, wave_shl:1 = 0x130,
+// row_bcast:15 = 0x142, row_bcast:31 = 0x143. Lanes whose source is out of
+// range, or outside row_mask, read 0.
+template <int kCtrl, int kRowMask = 0xF>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0u, uint32_t(v), kCtrl, kRowMask, 0xF, true);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0u, uint32_t(v >> 32), kCtrl, kRowMask, 0xF, true);
+    return uint64_t(lo) | (uint64_t(hi) << 32);
+}
+
+// Inclusive prefix sum over the 64 lanes: Kogge-Stone within each row of 16
+// (row_shr 1, 2, 4, 8), then the row totals carried by row_bcast:15 (rows 1,
+// 3) and row_bcast:31 (rows 2, 3). Six DPP steps on VALU instead of six
+// ds_bpermute round trips. Every lane must be active.
 __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
+    v += dpp_u64<0x111>(v);
+    v += dpp_u64<0x112>(v);
+    v += dpp_u64<0x114>(v);
+    v += dpp_u64<0x118>(v);
+    v += dpp_u64<0x142, 0xA>(v);
+    v += dpp_u64<0x143, 0xC>(v);
     return v;
 }
+
+// Value of lane l (wave-uniform l) in every lane: v_readlane into SGPRs.
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, int l) {
+    return uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), l))) |
+           (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), l))) << 32);
+}
+
+// Lane i receives lane i + 1's value (lane 63 receives 0): DPP wave_shl:1.
+__device__ __forceinline__ uint64_t next_lane_u64(uint64_t v) { return dpp_u64<0x130>(v); }
+
+// ---------------------------------------------------------------------------
+// Block-wide exclusive scan of u64 over 256 threads (4 waves)
+// ---------------------------------------------------------------------------
 
 // Returns the exclusive prefix of v within the block; *total = block sum.
 template <int NT>

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kLenThreads) void enc_len_kernel(EncArgs a) {
         const uint64_t incl = wave_incl_scan_u64(len);
         const uint64_t tile = (rw + 64 * k) / kEmitRecs;
         if (lane == 63 && tile * kEmitRecs < a.n) a.tile_sum[tile] = incl;
-        wsum += __shfl(incl, 63, 64);
+        wsum += lane_u64(incl, 63);
     }
     if (lane == 0) s_wave[wv] = wsum;
     __syncthreads();
@@ -129,9 +129,9 @@ __device__ __forceinline__ uint64_t tile_reduce(const TileLoads<kFused>& t, uint
     if (kFused) {
 #pragma unroll
         for (int k = 0; k < TileLoads<kFused>::kW; ++k) v += lane + 64ull * k < blk ? t.w[k] : 0;
-        return __shfl(wave_incl_scan_u64(v), 63, 64);
+        return lane_u64(wave_incl_scan_u64(v), 63);
     }
-    return t.w[0] + __shfl(wave_incl_scan_u64(v), 63, 64);
+    return t.w[0] + lane_u64(wave_incl_scan_u64(v), 63);
 }
 
 constexpr int kFastWaves = 4;                 // wave tiles per enc_emit workgroup
@@ -441,8 +441,8 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     const int64_t p0 = int64_t((pst + 15) >> 4);
     const int64_t p1 = max(p0, int64_t(en >> 4));
     const int64_t np = len ? p1 - p0 : 0;
-    const int64_t cfa_next = __shfl_down(cfa, 1, 64);
-    const int64_t cfa_end = int64_t((__shfl(en, nrec - 1, 64) + 15) >> 4);
+    const int64_t cfa_next = int64_t(next_lane_u64(uint64_t(cfa)));
+    const int64_t cfa_end = int64_t((lane_u64(en, nrec - 1) + 15) >> 4);
     const int64_t own_next = lane + 1 < nrec ? cfa_next : cfa_end;
     const uint32_t nonpure = lane < nrec && len ? uint32_t(own_next - cfa - np) : 0u;
     const uint64_t wnp = wave_incl_scan_u64(nonpure);
@@ -455,14 +455,14 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         // span: records [lo_rec, hi_rec) whose non-pure chunks (+1 for a
         // chunk shared with the record before) fit the image and whose bytes
         // fit kSpanBytesMax (at least one record)
-        const uint64_t wbase = lo_rec ? __shfl(wnp, lo_rec - 1, 64) : 0;
-        const uint64_t sbeg = __shfl(start, lo_rec, 64);
+        const uint64_t wbase = lo_rec ? lane_u64(wnp, lo_rec - 1) : 0;
+        const uint64_t sbeg = lane_u64(start, lo_rec);
         const uint64_t over = __ballot(lane > lo_rec && lane < nrec &&
                                        (wnp - wbase + 1 > uint64_t(kImgChunks) || en - sbeg > kSpanBytesMax));
         const int hi_rec = over ? min(nrec, int(__builtin_ctzll(over))) : nrec;
         const int ns = hi_rec - lo_rec;
         const uint64_t S0 = sbeg;
-        const uint64_t S1 = __shfl(en, hi_rec - 1, 64);
+        const uint64_t S1 = lane_u64(en, hi_rec - 1);
         const int64_t C0 = int64_t(S0 >> 4);
         const uint64_t B0 = uint64_t(C0) << 4;        // byte origin of the span-relative offsets
         if (lo_rec) wave_lds_sync();                   // the previous span's readers are done

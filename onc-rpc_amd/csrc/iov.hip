@@ -82,7 +82,7 @@ __global__ __launch_bounds__(64 * kIovWaves) void iov_emit_kernel(IovArgs a) {
     const uint64_t excl = incl - sv;
     const uint64_t wire_off = W0 + (excl >> 16);
     const uint64_t hoff = H0 + (excl & 0xFFFFu);        // byte offset in hdr_out
-    const uint64_t last = __shfl(incl, nrec - 1, 64);
+    const uint64_t last = lane_u64(incl, nrec - 1);
     const uint64_t Ht = last & 0xFFFFu;                  // header bytes of the tile
     const bool fits = hoff + hl <= a.hdr_cap;
     if (lane < nrec) {
