@@ -332,7 +332,7 @@ __device__ __forceinline__ void merge_chunk(const ChunkPlan& P, const uint32_t X
 // after the last step re-reads the last chunk). The one or two partial
 // chunks at the span's edges are written after the loop, with byte stores
 // of only the span's bytes.
-template <int kU, int kNT, bool kByte>
+template <int kU, int kNT, bool kByte, int kPipe = 2>
 __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, uint32_t gsh, uint64_t B0,
                                             uint64_t S0, uint64_t E, int32_t NCe, uintptr_t dummy) {
     const int lane = threadIdx.x & 63;
@@ -358,14 +358,34 @@ __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, 
         if (kNT & 2) __builtin_nontemporal_store(u32x4{v[0], v[1], v[2], v[3]}, d);  \
         else *d = u32x4{v[0], v[1], v[2], v[3]};                                          \
     }
-        ONC_ISSUE(Pa, Xa, La, cf);
-        for (int32_t st = cf;; st += 2 * S) {
-            ONC_ISSUE(Pb, Xb, Lb, st + S);
-            ONC_CONSUME(Pa, Xa, La, st);
-            if (st + S >= cl) break;
-            ONC_ISSUE(Pa, Xa, La, st + 2 * S);
-            ONC_CONSUME(Pb, Xb, Lb, st + S);
-            if (st + 2 * S >= cl) break;
+        if constexpr (kPipe == 3) {
+            // three register sets: two steps' loads in flight while one is consumed
+            ChunkPlan Pc[kU];
+            uint32_t Xc[kU][4];
+            uint4 Lc[kU];
+            ONC_ISSUE(Pa, Xa, La, cf);
+            ONC_ISSUE(Pb, Xb, Lb, cf + S);
+            for (int32_t st = cf;; st += 3 * S) {
+                ONC_ISSUE(Pc, Xc, Lc, st + 2 * S);
+                ONC_CONSUME(Pa, Xa, La, st);
+                if (st + S >= cl) break;
+                ONC_ISSUE(Pa, Xa, La, st + 3 * S);
+                ONC_CONSUME(Pb, Xb, Lb, st + S);
+                if (st + 2 * S >= cl) break;
+                ONC_ISSUE(Pb, Xb, Lb, st + 4 * S);
+                ONC_CONSUME(Pc, Xc, Lc, st + 2 * S);
+                if (st + 3 * S >= cl) break;
+            }
+        } else {
+            ONC_ISSUE(Pa, Xa, La, cf);
+            for (int32_t st = cf;; st += 2 * S) {
+                ONC_ISSUE(Pb, Xb, Lb, st + S);
+                ONC_CONSUME(Pa, Xa, La, st);
+                if (st + S >= cl) break;
+                ONC_ISSUE(Pa, Xa, La, st + 2 * S);
+                ONC_CONSUME(Pb, Xb, Lb, st + S);
+                if (st + 2 * S >= cl) break;
+            }
         }
 #undef ONC_ISSUE
 #undef ONC_CONSUME
@@ -387,7 +407,7 @@ __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, 
     }
 }
 
-template <int kU, int kNT, bool kFused>
+template <int kU, int kNT, bool kFused, int kPipe = 2>
 __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = tile * kEmitRecs;
@@ -516,7 +536,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         if (E <= S0) continue;                         // no bytes (all records failed, or beyond out_cap)
         const int32_t NCe = int32_t(((E + 15) >> 4) - C0);
         if (byte_mode) stream_span<1, kNT, true>(a, T, gsh, B0, S0, E, NCe, dummy);
-        else stream_span<kU, kNT, false>(a, T, gsh, B0, S0, E, NCe, dummy);
+        else stream_span<kU, kNT, false, kPipe>(a, T, gsh, B0, S0, E, NCe, dummy);
         if (lo_rec == hi_rec && hi_rec == nrec) ONC_PROF(4);
     }
     ONC_PROF(5);
@@ -527,11 +547,11 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
 // finds them cached, made the decode slower: 60 -> 69 us on c1, the dirty
 // lines are written back at the kernel boundary);
 // kOcc: workgroups per CU the register allocation must allow (0 = free)
-template <int kU, int kNT = 0, int kOcc = 0, bool kFused = false>
+template <int kU, int kNT = 0, int kOcc = 0, bool kFused = false, int kPipe = 2>
 __global__ __launch_bounds__(64 * kFastWaves, kOcc ? kOcc * kFastWaves / 4 : 1) void enc_emit_kernel_t(EncArgs a) {
     __shared__ ImgTile s_tiles[kFastWaves];
     const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
-    if (tile < num_emit_tiles(a.n)) enc_emit_tile<kU, kNT, kFused>(a, s_tiles[threadIdx.x >> 6], tile);
+    if (tile < num_emit_tiles(a.n)) enc_emit_tile<kU, kNT, kFused, kPipe>(a, s_tiles[threadIdx.x >> 6], tile);
 }
 
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
