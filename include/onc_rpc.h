@@ -310,6 +310,21 @@ int onc_encode(onc_codec* codec, const onc_batch* batch,
                uint8_t* out, uint64_t out_cap,
                uint64_t* rec_off, int32_t* status, uint32_t* rec_len);
 
+/* onc_encode in two phases on the handle's stream, so that the length pass
+ * of one batch can run while other work (the decode of the previous batch,
+ * on another stream) is in flight:
+ *   onc_encode_plan : serialised_len() + validation of every record
+ *                     (status, optional rec_len) and the placement totals,
+ *                     kept in this handle's scratch (enc_len);
+ *   onc_encode_emit : the bytes, placed by that plan (enc_emit) — same
+ *                     arguments and results as onc_encode.
+ * The plan belongs to the handle: emit must name the batch last planned on
+ * it (same msgs pointer and n, else ONC_RC_EINVAL), and the descriptors must
+ * not change in between. onc_encode = plan + emit. */
+int onc_encode_plan(onc_codec* codec, const onc_batch* batch, int32_t* status, uint32_t* rec_len);
+int onc_encode_emit(onc_codec* codec, const onc_batch* batch, uint8_t* out, uint64_t out_cap,
+                    uint64_t* rec_off, int32_t* status);
+
 /* Vectored encode (the zero-copy writer the reference
  * plans in README.md:71-75 and rpc_message.rs:19): only the header part of
  * every record (everything before the raw payload) is serialised, into

@@ -24,6 +24,9 @@ struct onc_codec {
     uint64_t frame_chunk = onc::kFrameChunkDefault;   // ONC_RPC_FRAME_CHUNK at create (bytes, >= 64)
     bool force_scan = false;   // ONC_RPC_FORCE_SCAN=1 at create: always launch the block scan (tests)
     uint32_t variant = 0;      // ONC_RPC_VARIANT at create: kernel variant bits (A/B measurements)
+    // the batch whose plan (onc_encode_plan) the scratch holds
+    const onc_msg* planned_msgs = nullptr;
+    uint64_t planned_n = ~0ull;
     uint32_t timing = 0;   // bitmask of ONC_K_* ids whose launches are bracketed
     struct Pending {
         int kernel;
@@ -95,6 +98,7 @@ int ensure_scratch(onc_codec* c, uint64_t tiles) {
         return ONC_RC_ENOMEM;
     }
     c->scratch_tiles = want;
+    c->planned_n = ~0ull;       // a plan in the old scratch is gone
     return ONC_RC_OK;
 }
 
@@ -299,6 +303,68 @@ int onc_encode_lengths(onc_codec* c, const onc_batch* batch, uint32_t* rec_len, 
     return run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
 }
 
+namespace {
+
+// Encoder arguments common to the plan and emit phases.
+int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* rec_len, onc::EncArgs& a) {
+    const uint64_t tiles = onc::num_emit_tiles(batch->n);
+    const int rc = ensure_scratch(c, tiles);
+    if (rc != ONC_RC_OK) return rc;
+    a = onc::EncArgs{};
+    a.n = batch->n;
+    a.msgs = batch->msgs;
+    a.unix = batch->unix_params;
+    a.auth_arena = batch->auth_arena;
+    a.payload_arena = batch->payload_arena;
+    a.bounds = bounds_of(batch);
+    a.status = status;
+    a.rec_len = rec_len;
+    bind_scratch(c, a);
+    // Up to kFusedBlocks enc_len workgroups (1M records), enc_emit sums the
+    // workgroup totals itself and the scan launch is skipped.
+    a.fused_base = onc::num_len_blocks(batch->n) <= onc::kFusedBlocks && !c->force_scan;
+    a.variant = c->variant;
+    return ONC_RC_OK;
+}
+
+// enc_len: plans + per-tile and per-workgroup byte totals into the scratch.
+int enc_plan(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* rec_len) {
+    onc::EncArgs a;
+    int rc = enc_args(c, batch, status, rec_len, a);
+    if (rc != ONC_RC_OK) return rc;
+    rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    c->planned_msgs = batch->msgs;
+    c->planned_n = batch->n;
+    return ONC_RC_OK;
+}
+
+// [scan of the workgroup totals, with the grand total into rec_off[n]] +
+// enc_emit: the bytes, placed by the plan in the scratch.
+int enc_emit(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
+             int32_t* status, uint32_t* rec_len) {
+    onc::EncArgs a;
+    int rc = enc_args(c, batch, status, rec_len, a);
+    if (rc != ONC_RC_OK) return rc;
+    // any writer position: the kernels work on 16-byte chunks from the
+    // aligned address below `out`, whose first `origin` bytes are never written
+    a.origin = reinterpret_cast<uintptr_t>(out) & 15;
+    a.out = out - a.origin;
+    a.out_cap = out ? a.origin + out_cap : 0;
+    a.rec_off = rec_off;
+    a.rec_len = nullptr;   // written by the plan
+    if (!a.fused_base) {
+        const uint64_t nblk = onc::num_len_blocks(batch->n);
+        rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
+            return onc::launch_scan_tiles(a.block_sum, a.block_base, nblk, 0, rec_off + batch->n, c->stream);
+        });
+        if (rc != ONC_RC_OK) return rc;
+    }
+    return run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
+}
+
+}  // namespace
+
 int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
                int32_t* status, uint32_t* rec_len) {
     if (!c || check_batch(batch) != ONC_RC_OK || !rec_off) return ONC_RC_EINVAL;
@@ -308,41 +374,35 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
         const hipError_t e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
         return e == hipSuccess ? ONC_RC_OK : fail(c, e, "hipMemsetAsync");
     }
-    const uint64_t tiles = onc::num_emit_tiles(batch->n);
-    int rc = ensure_scratch(c, tiles);
+    const int rc = enc_plan(c, batch, status, rec_len);
     if (rc != ONC_RC_OK) return rc;
-    onc::EncArgs a{};
-    a.n = batch->n;
-    a.msgs = batch->msgs;
-    a.unix = batch->unix_params;
-    a.auth_arena = batch->auth_arena;
-    a.payload_arena = batch->payload_arena;
-    a.bounds = bounds_of(batch);
-    // any writer position: the kernels work on 16-byte chunks from the
-    // aligned address below `out`, whose first `origin` bytes are never written
-    a.origin = reinterpret_cast<uintptr_t>(out) & 15;
-    a.out = out - a.origin;
-    a.out_cap = out ? a.origin + out_cap : 0;
-    a.rec_off = rec_off;
-    a.status = status;
-    a.rec_len = rec_len;
-    bind_scratch(c, a);
-    // enc_len: plans + tile/workgroup totals; scan: workgroup bases (and the
-    // grand total into rec_off[n]); enc_emit: the bytes.
-    // Up to kFusedBlocks workgroups, enc_emit sums the workgroup totals
-    // itself and the scan launch is skipped.
-    const uint64_t nblk = onc::num_len_blocks(batch->n);
-    a.fused_base = nblk <= onc::kFusedBlocks && !c->force_scan;
-    a.variant = c->variant;
-    rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
-    if (rc != ONC_RC_OK) return rc;
-    if (!a.fused_base) {
-        rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
-            return onc::launch_scan_tiles(a.block_sum, a.block_base, nblk, 0, rec_off + batch->n, c->stream);
-        });
-        if (rc != ONC_RC_OK) return rc;
+    return enc_emit(c, batch, out, out_cap, rec_off, status, nullptr);
+}
+
+int onc_encode_plan(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* rec_len) {
+    if (!c || check_batch(batch) != ONC_RC_OK) return ONC_RC_EINVAL;
+    if (batch->n && !status) return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    if (batch->n == 0) {
+        c->planned_msgs = batch->msgs;
+        c->planned_n = 0;
+        return ONC_RC_OK;
     }
-    return run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
+    return enc_plan(c, batch, status, rec_len);
+}
+
+int onc_encode_emit(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
+                    int32_t* status) {
+    if (!c || check_batch(batch) != ONC_RC_OK || !rec_off) return ONC_RC_EINVAL;
+    if (batch->n && (!status || (!out && out_cap))) return ONC_RC_EINVAL;
+    // the plan in this handle's scratch must be of this batch
+    if (c->planned_n != batch->n || c->planned_msgs != batch->msgs) return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    if (batch->n == 0) {
+        const hipError_t e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
+        return e == hipSuccess ? ONC_RC_OK : fail(c, e, "hipMemsetAsync");
+    }
+    return enc_emit(c, batch, out, out_cap, rec_off, status, nullptr);
 }
 
 int onc_encode_iov(onc_codec* c, const onc_batch* batch, uint8_t* hdr_out, uint64_t hdr_cap, onc_iov_rec* iov,

@@ -32,7 +32,7 @@ EXPORTED = [
     "onc_codec_sync", "onc_codec_reserve", "onc_codec_last_error", "onc_status_str",
     "onc_codec_enable_timing", "onc_codec_kernel_stats", "onc_codec_reset_stats",
     "onc_kernel_name", "onc_encode_lengths", "onc_encode", "onc_decode", "onc_scan_lengths",
-    "onc_expected_message_len", "onc_encode_iov", "onc_frame_stream",
+    "onc_expected_message_len", "onc_encode_iov", "onc_frame_stream", "onc_encode_plan", "onc_encode_emit",
 ]
 
 
@@ -77,6 +77,8 @@ def load_library(path=LIB_PATH):
     lib.onc_kernel_name.restype = C.c_char_p
     lib.onc_encode_lengths.argtypes = [vp, C.POINTER(OncBatch), vp, vp]
     lib.onc_encode.argtypes = [vp, C.POINTER(OncBatch), vp, u64, vp, vp, vp]
+    lib.onc_encode_plan.argtypes = [vp, C.POINTER(OncBatch), vp, vp]
+    lib.onc_encode_emit.argtypes = [vp, C.POINTER(OncBatch), vp, u64, vp, vp]
     lib.onc_decode.argtypes = [vp, vp, vp, u64, i32, C.POINTER(OncDecoded)]
     lib.onc_scan_lengths.argtypes = [vp, vp, u64, u64, vp]
     lib.onc_frame_stream.argtypes = [vp, vp, u64, vp, u64, vp]
@@ -212,6 +214,18 @@ class Codec:
         cap = out.numel() if out_cap is None else out_cap
         self._check(self.lib.onc_encode(self.h, C.byref(b), _ptr(out), cap, _ptr(rec_off), _ptr(status),
                                         _ptr(rec_len)), "onc_encode")
+
+    def encode_plan(self, batch: DeviceBatch, status, rec_len=None):
+        """Phase 1 of onc_encode (enc_len): lengths, validation, placement totals."""
+        b = batch.c_struct()
+        self._check(self.lib.onc_encode_plan(self.h, C.byref(b), _ptr(status), _ptr(rec_len)), "onc_encode_plan")
+
+    def encode_emit(self, batch: DeviceBatch, out, rec_off, status, out_cap=None):
+        """Phase 2 of onc_encode (enc_emit) of the batch last planned on this handle."""
+        b = batch.c_struct()
+        cap = out.numel() if out_cap is None else out_cap
+        self._check(self.lib.onc_encode_emit(self.h, C.byref(b), _ptr(out), cap, _ptr(rec_off), _ptr(status)),
+                    "onc_encode_emit")
 
     def encode_iov(self, batch: DeviceBatch, hdr_out, iov, status, totals=None, hdr_cap=None):
         """Vectored encode: headers into hdr_out, one onc_iov_rec (32 B) per record in iov."""

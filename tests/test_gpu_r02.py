@@ -342,3 +342,32 @@ def test_scan_lengths_sizes_and_alignment(R, force):
             got = off[oshift:].cpu().numpy().view(np.uint64)
             assert np.array_equal(got, want), (n, lshift, oshift, np.nonzero(got != want)[0][:5])
     c.close()
+
+
+def test_encode_plan_emit(codec, R, oracle):
+    """onc_encode in two phases (onc_encode_plan = enc_len, onc_encode_emit =
+    enc_emit): the same bytes, offsets and statuses as onc_encode and the
+    oracle, at any writer position, the plan reusable for several emits;
+    an emit of a batch that is not the handle's last plan is refused."""
+    import torch
+    hb = S.mixed(1500, seed=19, pmin=0, pmax=500, exotic=0.2)
+    o_wire, o_off, o_st, o_len = oracle.encode_batch(hb)
+    db = R.DeviceBatch.from_host(hb)
+    total = len(o_wire)
+    st = torch.empty(hb.n, dtype=torch.int32, device="cuda")
+    rl = torch.empty(hb.n, dtype=torch.int32, device="cuda")
+    codec.encode_plan(db, st, rl)
+    codec.sync()
+    assert np.array_equal(rl.cpu().numpy().view(np.uint32), o_len)
+    for shift in (0, 5):
+        buf = torch.full((total + shift + 32,), 0x5A, dtype=torch.uint8, device="cuda")
+        off = torch.empty(hb.n + 1, dtype=torch.int64, device="cuda")
+        codec.encode_emit(db, buf[shift:], off, st, out_cap=total)
+        codec.sync()
+        b = buf.cpu().numpy()
+        assert b[shift:shift + total].tobytes() == o_wire and (b[:shift] == 0x5A).all()
+        assert np.array_equal(off.cpu().numpy().view(np.uint64), o_off)
+        assert np.array_equal(st.cpu().numpy(), o_st)
+    other = R.DeviceBatch.from_host(S.call_none(10, 16))
+    with pytest.raises(R.CodecError):
+        codec.encode_emit(other, buf, off, st)
