@@ -405,7 +405,7 @@ def pcie_pipelined(args, torch, R, wl, hb, db, out, total_bytes, lens_np, rec_le
             wb = int(pref[hi] - pref[lo])
             if not torch.equal(h_wire[base[k]:base[k] + wb], ref[int(pref[lo]):int(pref[hi])]):
                 ok = False
-    pt = torch.tensor([pms, 0.0 if ok else 1.0], dtype=torch.float64, device=out.device)
+    pt = torch.tensor([pms, 0.0 if ok else 1.0], dtype=torch.float64, device=cdev(out.device))
     if dist is not None:
         dist.all_reduce(pt, op=dist.ReduceOp.MAX)
     pms = float(pt[0])
@@ -421,6 +421,15 @@ def pcie_pipelined(args, torch, R, wl, hb, db, out, total_bytes, lens_np, rec_le
 # ---------------------------------------------------------------------------
 # timing + roofline (shared by every workload)
 # ---------------------------------------------------------------------------
+BACKEND = ["nccl"]
+
+
+def cdev(dev):
+    """Device of the control-plane collective tensors: the GPU under RCCL
+    (`nccl`), the host under gloo."""
+    return dev if BACKEND[0] == "nccl" else "cpu"
+
+
 ALG_PER_LAUNCH = {
     # algorithmic bytes per launch (SURVEY §8(d)): encode reads ~W and writes
     # W; zero-copy decode reads H + 4 (the length) and writes ~H.
@@ -553,7 +562,7 @@ def breakdown_dict(tm, n, sum_W, sum_H):
 
 def gather_per_gpu(torch, dist, dev, rank, n, ms_per_step, ms_clean_per_step):
     """[records, ms/step, event-free ms/step] of every rank (control plane)."""
-    t = torch.tensor([float(n), ms_per_step, ms_clean_per_step], dtype=torch.float64, device=dev)
+    t = torch.tensor([float(n), ms_per_step, ms_clean_per_step], dtype=torch.float64, device=cdev(dev))
     if dist is None:
         rows = [t]
     else:
@@ -569,7 +578,7 @@ def gather_per_gpu(torch, dist, dev, rank, n, ms_per_step, ms_clean_per_step):
 
 def agree(torch, dist, dev, ok):
     """Every rank's flag, AND-ed (one collective all ranks always reach)."""
-    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev(dev))
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(t.item())
@@ -607,7 +616,7 @@ def run_c4(args, torch, R, S, SH, L, dist, rank, world, local_rank, total, mode,
             dist.barrier()
 
     tm = Timing(torch, R, codec, step, steps, warmup, barrier)
-    t = torch.tensor([tm.ms, tm.ms_clean], dtype=torch.float64, device=dev)
+    t = torch.tensor([tm.ms, tm.ms_clean], dtype=torch.float64, device=cdev(dev))
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ms_max, ms_clean_max = float(t[0]), float(t[1])
@@ -724,7 +733,7 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
             dist.barrier()
 
     tm = Timing(torch, R, codec, step, args.steps, args.warmup, barrier)
-    t = torch.tensor([tm.ms, tm.ms_clean], dtype=torch.float64, device=dev)
+    t = torch.tensor([tm.ms, tm.ms_clean], dtype=torch.float64, device=cdev(dev))
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ms_max, ms_clean_max = float(t[0]), float(t[1])
@@ -777,7 +786,7 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
         e5.record()
         torch.cuda.synchronize()
         pms = e4.elapsed_time(e5) / args.pcie_reps
-        pt = torch.tensor([pms], dtype=torch.float64, device=dev)
+        pt = torch.tensor([pms], dtype=torch.float64, device=cdev(dev))
         if dist is not None:
             dist.all_reduce(pt, op=dist.ReduceOp.MAX)
         pms = float(pt[0])
@@ -848,6 +857,9 @@ def main():
     world = int(world_env or "1")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("ONC_BENCH_SAME_DEVICE") == "1":
+        # lab: every rank on GPU 0 (exercises the multi-rank path on a 1-GPU box; use --backend gloo)
+        local_rank = 0
     if args.gpus is None:
         args.gpus = world
     if args.gpus != world:
@@ -870,6 +882,7 @@ def main():
     torch.cuda.set_device(local_rank)
     if world > 1:
         import torch.distributed as dist
+        BACKEND[0] = args.backend
         dist.init_process_group(args.backend)
         if dist.get_world_size() != args.gpus:
             sys.exit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
