@@ -505,7 +505,8 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                 // the record's non-pure bytes are contiguous in the image from
                 // image byte start - 16 (C0 + NP)
                 const uint64_t ibb = start - 16ull * uint64_t(C0 + NP);
-                // reloaded (an L2 hit) rather than kept live across the span loop
+                // reloaded (an L2 hit) rather than kept live across the span
+                // loop (kept live: 162 VGPRs, 3 waves per SIMD)
                 MsgRegs mr2 = issue_msg(a.msgs + r0 + lane);
                 asm volatile("" : "+v"(mr2.q[0]), "+v"(mr2.q[1]), "+v"(mr2.q[2]), "+v"(mr2.q[3]));
                 const onc_msg d = as_msg(mr2);
