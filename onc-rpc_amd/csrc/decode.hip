@@ -75,6 +75,17 @@ struct Rules {
 // AUTH_UNIX verifier (written after the credential, so it wins).
 //   pad: 1 = credential slot (zeros after it), 2 = verifier slot whose
 //   credential slot is unused (zeros before it), 0 = no padding.
+// Output stores: the decoded descriptors (staged through LDS, 16 KiB
+// contiguous per workgroup) and the status / aux arrays fill whole lines
+// and are stored nontemporally — the decoder never reads them back, and
+// plain stores leave dirty lines for the next kernel to write back
+// (measured: c1 step +2-3 %, c3 +2 %; tools/store_lab.hip for the
+// mechanism). AUTH_UNIX slots are written lane by lane (192 bytes at a
+// 192-byte stride) and keep plain stores: L2 merges the neighbouring
+// lanes' pieces into whole lines, where nontemporal stores send each piece
+// to memory as a partial line (c3 decode 450 -> 1040-1300 us); for sparse
+// slots (configs[2]: a quarter of the records) the two policies measured
+// within the run-to-run spread.
 __device__ __forceinline__ void put_unix(onc_unix_params* u, uint32_t stamp, uint32_t uid, uint32_t gid,
                                          uint32_t ng, uint64_t name_off, uint32_t nl, const uint32_t* gids,
                                          uint32_t pad) {
@@ -320,7 +331,7 @@ __device__ __forceinline__ int32_t parse_record(const Rd& R, uint64_t L, uint64_
 // (tools/dec_lab.hip: 1 / 2 / 3 / 4 chunks per record, 1M records 300 B
 // apart, cold: 53 / 59 / 65 / 71 us — ~53 us per million lines). Measured
 // c1 decode 59.6 -> 56.0 us, c2 90.1 -> 88.5 us, c3 unchanged.
-template <int MODE, bool kExact = false>
+template <int MODE, bool kExact = false, bool kNTOut = false>
 __global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
     __shared__ uint32_t s_win[kWinWords * kTile];
     static_assert(kWinWords * kTile * 4 >= kTile * sizeof(onc_msg), "descriptor staging reuses the window");
@@ -415,9 +426,15 @@ __global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);
         }
-        a.out.status[i] = st;
-        a.out.aux0[i] = aux0;
-        a.out.aux1[i] = aux1;
+        if (kNTOut) {
+            __builtin_nontemporal_store(st, a.out.status + i);
+            __builtin_nontemporal_store(aux0, a.out.aux0 + i);
+            __builtin_nontemporal_store(aux1, a.out.aux1 + i);
+        } else {
+            a.out.status[i] = st;
+            a.out.aux0[i] = aux0;
+            a.out.aux1[i] = aux1;
+        }
     }
     __syncthreads();                                  // every lane is done with its window
     uint4* stage = reinterpret_cast<uint4*>(s_win);
@@ -429,16 +446,22 @@ __global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t j = uint32_t(k * kTile + t);
-        if (j < 4 * nblk) dst[j] = stage[j];
+        if (j < 4 * nblk) {
+            if (kNTOut) {
+                const uint4 v = stage[j];
+                __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst + j));
+            }
+            else dst[j] = stage[j];
+        }
     }
 }
 
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s) {
     const uint64_t tiles = num_tiles(a.n);
     if (mode == ONC_DECODE_BYTES)
-        hipLaunchKernelGGL((decode_kernel<ONC_DECODE_BYTES, true>), dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
+        hipLaunchKernelGGL((decode_kernel<ONC_DECODE_BYTES, true, true>), dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
     else
-        hipLaunchKernelGGL((decode_kernel<ONC_DECODE_SLICE, true>), dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
+        hipLaunchKernelGGL((decode_kernel<ONC_DECODE_SLICE, true, true>), dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
     return hipGetLastError();
 }
 
