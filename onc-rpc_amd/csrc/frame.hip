@@ -411,6 +411,46 @@ __global__ __launch_bounds__(64) void frame_walk_kernel(FrameArgs a) {
     }
 }
 
+// Records of chunk t that belong to the framed stream, summed per block of
+// kCntBlk chunks (one per thread: a 2 GB stream is only 30k chunks, so the
+// grid stays wide): the counts kernel and the first level of the count scan
+// in one launch. frame_coff then gives every chunk its first record index
+// (each block sums the block totals before it itself).
+constexpr uint64_t kCntBlk = 256;
+constexpr uint64_t kCntBlkMax = 2048;   // 512k chunks (32 GiB of stream at 64 KiB); beyond: the 3-launch scan
+
+__device__ __forceinline__ uint32_t cnt_eff_of(const FrameArgs& a, uint64_t t, uint64_t stop) {
+    return (t < a.nchunks && a.g[t] != kNone && t <= stop) ? a.cnt[t] : 0u;
+}
+
+__global__ __launch_bounds__(256) void frame_cblk_kernel(FrameArgs a, uint64_t* blk_sum) {
+    __shared__ uint64_t s_wave[4];
+    const uint64_t stop = *a.first_stop;
+    const uint64_t t = uint64_t(blockIdx.x) * kCntBlk + threadIdx.x;
+    const uint32_t ce = cnt_eff_of(a, t, stop);
+    if (t < a.nchunks) a.cnt_eff[t] = ce;
+    uint64_t total;
+    block_excl_scan_u64<256>(ce, s_wave, &total);
+    if (threadIdx.x == 0) blk_sum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void frame_coff_kernel(FrameArgs a, const uint64_t* blk_sum) {
+    __shared__ uint64_t s_wave[4];
+    const uint64_t b = blockIdx.x;
+    const uint64_t t = b * kCntBlk + threadIdx.x;
+    const uint32_t v = t < a.nchunks ? a.cnt_eff[t] : 0u;
+    uint64_t pre = 0;
+#pragma unroll
+    for (int k = 0; k < int(kCntBlkMax / 256); ++k) {
+        const uint64_t j = uint64_t(threadIdx.x) + uint64_t(k) * 256;
+        if (j < b) pre += blk_sum[j];
+    }
+    uint64_t pre_total, total;
+    block_excl_scan_u64<256>(pre, s_wave, &pre_total);
+    const uint64_t run = pre_total + block_excl_scan_u64<256>(v, s_wave, &total);
+    if (t < a.nchunks) a.cnt_base[t] = run;
+}
+
 // Records of chunk t that belong to the framed stream.
 __global__ __launch_bounds__(256) void frame_counts_kernel(FrameArgs a) {
     const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -427,6 +467,46 @@ __device__ __forceinline__ void put_result(const FrameArgs& a, uint64_t n, uint6
     a.result[2] = uint64_t(int64_t(st));
     a.result[3] = aux0;
     a.result[4] = aux1;
+}
+
+// rec_off from the kept starts: a wave per chunk, lane i copies the chunk's
+// record i (coalesced 8-byte stores of consecutive records); a chunk with
+// more than kStartsCap records is re-chased by its lane 0 (small records).
+__global__ __launch_bounds__(256) void frame_write_slots_kernel(FrameArgs a) {
+    const uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    const uint32_t i = threadIdx.x & 63;
+    if (t >= a.nchunks) return;
+    const uint32_t ce = a.cnt_eff[t];
+    const uint64_t k0 = a.cnt_base[t];
+    if (ce != 0 && k0 <= a.max_records) {
+        const uint64_t* rec = a.starts + t * kStartsCap;
+        if (ce <= kStartsCap) {
+            if (i < ce) {
+                const uint64_t k = k0 + i;
+                const uint64_t p = rec[i];
+                if (k < a.max_records) a.rec_off[k] = p;
+                else if (k == a.max_records) put_result(a, k, p, ONC_OK, 0, 0);   // record max_records is not framed
+            }
+        } else if (i == 0) {
+            const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
+            uint64_t p = a.g[t];
+            for (uint32_t j = 0; j < ce; ++j) {
+                const uint64_t k = k0 + j;
+                if (k == a.max_records) {
+                    put_result(a, k, p, ONC_OK, 0, 0);
+                    break;
+                }
+                a.rec_off[k] = p;
+                p += uint64_t(be_at(base, p) & 0x7FFFFFFFu) + 4;
+            }
+        }
+    }
+    if (i == 0 && t == *a.first_stop) {
+        const uint64_t n = k0 + ce;
+        // reaching max_records ends the caller's loop before it looks further
+        if (n < a.max_records) put_result(a, n, a.x[t], a.st[t], a.aux[2 * t], a.aux[2 * t + 1]);
+        else if (n == a.max_records) put_result(a, n, a.x[t], ONC_OK, 0, 0);
+    }
 }
 
 __global__ __launch_bounds__(256) void frame_write_kernel(FrameArgs a) {
@@ -479,6 +559,25 @@ hipError_t launch_frame_verify(const FrameArgs& a, hipStream_t s) {
 
 hipError_t launch_frame_walk(const FrameArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(frame_walk_kernel, dim3(1), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+bool frame_fused_scan_ok(uint64_t nchunks) { return (nchunks + kCntBlk - 1) / kCntBlk <= kCntBlkMax; }
+
+hipError_t launch_frame_cblk(const FrameArgs& a, uint64_t* blk_sum, hipStream_t s) {
+    hipLaunchKernelGGL(frame_cblk_kernel, dim3(uint32_t((a.nchunks + kCntBlk - 1) / kCntBlk)), dim3(256), 0, s, a,
+                       blk_sum);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_coff(const FrameArgs& a, const uint64_t* blk_sum, hipStream_t s) {
+    hipLaunchKernelGGL(frame_coff_kernel, dim3(uint32_t((a.nchunks + kCntBlk - 1) / kCntBlk)), dim3(256), 0, s, a,
+                       blk_sum);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_write_slots(const FrameArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(frame_write_slots_kernel, dim3(uint32_t((a.nchunks + 3) / 4)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

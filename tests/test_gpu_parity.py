@@ -571,15 +571,19 @@ def _frame_both(R, codec, oracle, buf, max_records=None):
     return o
 
 
-@pytest.fixture(params=[None, 64, 1024])
+@pytest.fixture(params=[None, 64, 1024, "force_scan"])
 def frame_codec(request, R, monkeypatch):
     """Codec with the default framing chunk (64 KiB) and with small chunks
     (ONC_RPC_FRAME_CHUNK), so that test streams span many chunks: guesses,
-    verification and the walk across chunk boundaries."""
-    if request.param is not None:
+    verification and the walk across chunk boundaries; "force_scan" takes the
+    three-launch count scan (ONC_RPC_FORCE_SCAN=1) instead of the fused one."""
+    if request.param == "force_scan":
+        monkeypatch.setenv("ONC_RPC_FORCE_SCAN", "1")
+    elif request.param is not None:
         monkeypatch.setenv("ONC_RPC_FRAME_CHUNK", str(request.param))
     c = R.Codec(0)
     monkeypatch.delenv("ONC_RPC_FRAME_CHUNK", raising=False)
+    monkeypatch.delenv("ONC_RPC_FORCE_SCAN", raising=False)
     yield c
     c.close()
 
