@@ -459,9 +459,9 @@ __global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s) {
     const uint64_t tiles = num_tiles(a.n);
     if (mode == ONC_DECODE_BYTES)
-        hipLaunchKernelGGL((decode_kernel<ONC_DECODE_BYTES, true, true>), dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
+        ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true>), dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
     else
-        hipLaunchKernelGGL((decode_kernel<ONC_DECODE_SLICE, true, true>), dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
+        ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true>), dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
     return hipGetLastError();
 }
 

@@ -556,17 +556,17 @@ __global__ __launch_bounds__(64 * kFastWaves, kOcc ? kOcc * kFastWaves / 4 : 1) 
 }
 
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(enc_len_kernel, dim3(uint32_t(num_len_blocks(a.n))), dim3(kLenThreads), 0, s, a);
+    ONC_LAUNCH(enc_len_kernel, dim3(uint32_t(num_len_blocks(a.n))), dim3(kLenThreads), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
     const uint64_t blocks = (num_emit_tiles(a.n) + kFastWaves - 1) / kFastWaves;
     if (a.fused_base)
-        hipLaunchKernelGGL((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, true>), dim3(uint32_t(blocks)),
+        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, true>), dim3(uint32_t(blocks)),
                            dim3(64 * kFastWaves), 0, s, a);
     else
-        hipLaunchKernelGGL((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, false>), dim3(uint32_t(blocks)),
+        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, false>), dim3(uint32_t(blocks)),
                            dim3(64 * kFastWaves), 0, s, a);
     return hipGetLastError();
 }

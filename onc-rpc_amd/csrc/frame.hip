@@ -541,55 +541,55 @@ __global__ __launch_bounds__(256) void frame_write_kernel(FrameArgs a) {
 
 hipError_t launch_frame_guess(const FrameArgs& a, hipStream_t s) {
     const uint64_t waves = (a.nchunks + kGuessSub - 1) / kGuessSub;
-    hipLaunchKernelGGL(frame_guess_kernel, dim3(uint32_t((waves + 3) / 4)), dim3(256), 0, s, a);
+    ONC_LAUNCH(frame_guess_kernel, dim3(uint32_t((waves + 3) / 4)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_frame_chunks(const FrameArgs& a, hipStream_t s) {
     const uint32_t blocks = uint32_t((a.nchunks + 255) / 256);
-    hipLaunchKernelGGL(frame_chunks_kernel, dim3(blocks), dim3(256), 0, s, a);
+    ONC_LAUNCH(frame_chunks_kernel, dim3(blocks), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_frame_verify(const FrameArgs& a, hipStream_t s) {
     const uint32_t blocks = uint32_t((a.nchunks + 255) / 256);
-    hipLaunchKernelGGL(frame_verify_kernel, dim3(blocks), dim3(256), 0, s, a);
+    ONC_LAUNCH(frame_verify_kernel, dim3(blocks), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_frame_walk(const FrameArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(frame_walk_kernel, dim3(1), dim3(64), 0, s, a);
+    ONC_LAUNCH(frame_walk_kernel, dim3(1), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 
 bool frame_fused_scan_ok(uint64_t nchunks) { return (nchunks + kCntBlk - 1) / kCntBlk <= kCntBlkMax; }
 
 hipError_t launch_frame_cblk(const FrameArgs& a, uint64_t* blk_sum, hipStream_t s) {
-    hipLaunchKernelGGL(frame_cblk_kernel, dim3(uint32_t((a.nchunks + kCntBlk - 1) / kCntBlk)), dim3(256), 0, s, a,
+    ONC_LAUNCH(frame_cblk_kernel, dim3(uint32_t((a.nchunks + kCntBlk - 1) / kCntBlk)), dim3(256), 0, s, a,
                        blk_sum);
     return hipGetLastError();
 }
 
 hipError_t launch_frame_coff(const FrameArgs& a, const uint64_t* blk_sum, hipStream_t s) {
-    hipLaunchKernelGGL(frame_coff_kernel, dim3(uint32_t((a.nchunks + kCntBlk - 1) / kCntBlk)), dim3(256), 0, s, a,
+    ONC_LAUNCH(frame_coff_kernel, dim3(uint32_t((a.nchunks + kCntBlk - 1) / kCntBlk)), dim3(256), 0, s, a,
                        blk_sum);
     return hipGetLastError();
 }
 
 hipError_t launch_frame_write_slots(const FrameArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(frame_write_slots_kernel, dim3(uint32_t((a.nchunks + 3) / 4)), dim3(256), 0, s, a);
+    ONC_LAUNCH(frame_write_slots_kernel, dim3(uint32_t((a.nchunks + 3) / 4)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_frame_counts(const FrameArgs& a, hipStream_t s) {
     const uint32_t blocks = uint32_t((a.nchunks + 255) / 256);
-    hipLaunchKernelGGL(frame_counts_kernel, dim3(blocks), dim3(256), 0, s, a);
+    ONC_LAUNCH(frame_counts_kernel, dim3(blocks), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_frame_write(const FrameArgs& a, hipStream_t s) {
     const uint32_t blocks = uint32_t((a.nchunks + 255) / 256);
-    hipLaunchKernelGGL(frame_write_kernel, dim3(blocks), dim3(256), 0, s, a);
+    ONC_LAUNCH(frame_write_kernel, dim3(blocks), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -126,13 +126,13 @@ __global__ __launch_bounds__(64 * kIovWaves) void iov_emit_kernel(IovArgs a) {
 }
 
 hipError_t launch_iov_len(const IovArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(iov_len_kernel, dim3(uint32_t(num_tiles(a.n))), dim3(kTile), 0, s, a);
+    ONC_LAUNCH(iov_len_kernel, dim3(uint32_t(num_tiles(a.n))), dim3(kTile), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_iov_emit(const IovArgs& a, hipStream_t s) {
     const uint64_t blocks = (num_emit_tiles(a.n) + kIovWaves - 1) / kIovWaves;
-    hipLaunchKernelGGL(iov_emit_kernel, dim3(uint32_t(blocks)), dim3(64 * kIovWaves), 0, s, a);
+    ONC_LAUNCH(iov_emit_kernel, dim3(uint32_t(blocks)), dim3(64 * kIovWaves), 0, s, a);
     return hipGetLastError();
 }
 

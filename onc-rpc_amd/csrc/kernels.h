@@ -2,6 +2,7 @@
 // shared library; the public surface is include/onc_rpc.h).
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -9,6 +10,29 @@
 #include "common.h"
 
 namespace onc {
+
+// Per-kernel timing (onc_codec_enable_timing): codec.hip's run() hands the
+// start/stop events to the next launch, which then goes through
+// hipExtLaunchKernelGGL — the events take the dispatch packet's own
+// timestamps instead of marker packets recorded around it (each marker
+// pair serialised the stream: ~7 us per timed launch on gfx950).
+struct LaunchEvents {
+    hipEvent_t start, stop;
+};
+extern thread_local LaunchEvents t_launch_events;
+inline LaunchEvents take_launch_events() {
+    const LaunchEvents e = t_launch_events;
+    t_launch_events = LaunchEvents{nullptr, nullptr};
+    return e;
+}
+#define ONC_LAUNCH(K, G, B, L, S, ...)                                                               \
+    do {                                                                                             \
+        const ::onc::LaunchEvents ev_ = ::onc::take_launch_events();                                 \
+        if (ev_.start)                                                                               \
+            hipExtLaunchKernelGGL(K, G, B, L, S, ev_.start, ev_.stop, 0, __VA_ARGS__);               \
+        else                                                                                         \
+            hipLaunchKernelGGL(K, G, B, L, S, __VA_ARGS__);                                          \
+    } while (0)
 
 struct EncArgs {
     uint64_t n;

@@ -163,19 +163,19 @@ __global__ __launch_bounds__(kTile) void lenoff_kernel(const uint32_t* len, uint
 
 hipError_t launch_scan_tiles(const uint64_t* in, uint64_t* out_excl, uint64_t count, uint64_t base,
                              uint64_t* total_out, hipStream_t s) {
-    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(kScanThreads), 0, s, in, out_excl, count, base,
+    ONC_LAUNCH(scan_tiles_kernel, dim3(1), dim3(kScanThreads), 0, s, in, out_excl, count, base,
                        total_out);
     return hipGetLastError();
 }
 
 hipError_t launch_len_tiles(const uint32_t* len, uint64_t n, uint64_t* tile_sum, hipStream_t s) {
-    hipLaunchKernelGGL(len_tiles_kernel, dim3(uint32_t(num_tiles(n))), dim3(kTile), 0, s, len, n, tile_sum);
+    ONC_LAUNCH(len_tiles_kernel, dim3(uint32_t(num_tiles(n))), dim3(kTile), 0, s, len, n, tile_sum);
     return hipGetLastError();
 }
 
 hipError_t launch_len_apply(const uint32_t* len, uint64_t n, const uint64_t* tile_base, uint64_t* rec_off,
                             hipStream_t s) {
-    hipLaunchKernelGGL(len_apply_kernel, dim3(uint32_t(num_tiles(n))), dim3(kTile), 0, s, len, n, tile_base,
+    ONC_LAUNCH(len_apply_kernel, dim3(uint32_t(num_tiles(n))), dim3(kTile), 0, s, len, n, tile_base,
                        rec_off);
     return hipGetLastError();
 }
@@ -183,13 +183,13 @@ hipError_t launch_len_apply(const uint32_t* len, uint64_t n, const uint64_t* til
 bool scan_lengths_fused_ok(uint64_t n) { return (n + kLenBlk - 1) / kLenBlk <= kLenBlkMax; }
 
 hipError_t launch_lenblk(const uint32_t* len, uint64_t n, uint64_t* blk_sum, hipStream_t s) {
-    hipLaunchKernelGGL(lenblk_kernel, dim3(uint32_t((n + kLenBlk - 1) / kLenBlk)), dim3(kTile), 0, s, len, n, blk_sum);
+    ONC_LAUNCH(lenblk_kernel, dim3(uint32_t((n + kLenBlk - 1) / kLenBlk)), dim3(kTile), 0, s, len, n, blk_sum);
     return hipGetLastError();
 }
 
 hipError_t launch_lenoff(const uint32_t* len, uint64_t n, const uint64_t* blk_sum, uint64_t base, uint64_t* rec_off,
                          hipStream_t s) {
-    hipLaunchKernelGGL(lenoff_kernel, dim3(uint32_t((n + kLenBlk - 1) / kLenBlk)), dim3(kTile), 0, s, len, n, blk_sum,
+    ONC_LAUNCH(lenoff_kernel, dim3(uint32_t((n + kLenBlk - 1) / kLenBlk)), dim3(kTile), 0, s, len, n, blk_sum,
                        base, rec_off);
     return hipGetLastError();
 }

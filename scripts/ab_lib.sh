@@ -9,5 +9,5 @@ fi
 for r in 1 2; do for wl in ${WLS:-c1 c3}; do for lv in ${LIBS}; do
   name=${lv%%:*}; lib=${lv#*:}
   ONC_RPC_AMD_LIB=$PWD/$lib timeout -k 10 200 python bench.py --workload $wl --no-cpu-baseline --no-pcie --c4-leg off ${BARGS:-} > gpurun_out/ab/${wl}_${name}_r$r.log 2>&1 || exit $?
-  python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[1].split('/')[-1], round(d['value'],1), round(d['ms_per_step']*1e3,1), {k.replace('_kernel',''):round(v['avg_us'],1) for k,v in d['kernels_breakdown_pass'].items()})" gpurun_out/ab/${wl}_${name}_r$r.log
+  python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[1].split('/')[-1], round(d['value'],1), round(d['ms_per_step']*1e3,1), round(d['ms_per_step_without_kernel_events']*1e3,1), 'dom', round(d['roofline']['avg_launch_us'],1), {k.replace('_kernel',''):round(v['avg_us'],1) for k,v in d['kernels_breakdown_pass'].items()})" gpurun_out/ab/${wl}_${name}_r$r.log
 done; done; done
