@@ -371,3 +371,42 @@ def test_encode_plan_emit(codec, R, oracle):
     other = R.DeviceBatch.from_host(S.call_none(10, 16))
     with pytest.raises(R.CodecError):
         codec.encode_emit(other, buf, off, st)
+
+
+def test_kernel_timing(R, oracle):
+    """onc_codec_enable_timing / onc_codec_kernel_stats (the bench's
+    measurement path: timed launches go through hipExtLaunchKernelGGL with
+    start/stop events): every launch of a timed kernel is counted with a
+    positive duration, a mask times only its kernels, stats reset, and the
+    outputs are the same as untimed and bit-exact."""
+    hb = S.mixed(6000, seed=21, pmin=0, pmax=600, exotic=0.1)
+    o_wire, o_off, o_st, _ = oracle.encode_batch(hb)
+    c = R.Codec(0)
+    try:
+        plain = R.encode_host_batch(c, hb)
+        dec_plain = R.decode_host_wire(c, np.frombuffer(plain[0] + b"\0" * 16, np.uint8), plain[1], L.DECODE_SLICE)
+        c.enable_timing(True)
+        timed = R.encode_host_batch(c, hb)
+        dec_timed = R.decode_host_wire(c, np.frombuffer(timed[0] + b"\0" * 16, np.uint8), timed[1], L.DECODE_SLICE)
+        st = c.kernel_stats()
+        # encode_host_batch: lengths pass (enc_len) + encode (enc_len, enc_emit)
+        assert st["enc_len_kernel"][1] == 2 and st["enc_len_kernel"][0] > 0, st
+        assert st["enc_emit_kernel"][1] == 1 and st["enc_emit_kernel"][0] > 0, st
+        assert st["decode_kernel"][1] == 1 and st["decode_kernel"][0] > 0, st
+        assert timed[0] == plain[0] == o_wire
+        assert np.array_equal(timed[1], o_off) and np.array_equal(timed[2], o_st)
+        for x, y in zip(dec_timed, dec_plain):
+            assert np.array_equal(x, y)
+        c.reset_stats()
+        c.enable_timing(True, kernels=[R.K_ENC_EMIT])
+        R.encode_host_batch(c, hb)
+        R.decode_host_wire(c, np.frombuffer(plain[0] + b"\0" * 16, np.uint8), plain[1], L.DECODE_SLICE)
+        st = c.kernel_stats()
+        assert st["enc_emit_kernel"][1] == 1
+        assert all(v[1] == 0 for k, v in st.items() if k != "enc_emit_kernel"), st
+        c.enable_timing(False)
+        c.reset_stats()
+        R.encode_host_batch(c, hb)
+        assert all(v[1] == 0 for v in c.kernel_stats().values())
+    finally:
+        c.close()
