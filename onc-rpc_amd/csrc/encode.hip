@@ -172,7 +172,15 @@ constexpr int kFastWaves = 4;                 // wave tiles per enc_emit workgro
 // neighbours own the other bytes), the payload load is a dwordx4 + dword
 // at the 4-aligned address below the window + v_alignbyte, then a byte
 // rotation and a byte-masked merge (v_bfi).
-constexpr int kImgChunks = 248;               // image capacity per span (3968 B: 6 workgroups per CU)
+// Image capacity per span: 320 chunks (7.7 KiB per wave with the entries and
+// the map; 4 workgroups of 4 waves per CU, the VGPR limit, use 123 KiB of
+// LDS). A tile of 64 configs[0]-shaped records (AUTH_UNIX with 16 gids,
+// ~9 header chunks each: 576) streams in 2 spans instead of 3 at 248:
+// enc_emit 126 -> 117 us on c0; c1 (~4 per record) is one span either way.
+#ifndef ONC_IMG_CHUNKS
+#define ONC_IMG_CHUNKS 320
+#endif
+constexpr int kImgChunks = ONC_IMG_CHUNKS;
 #ifndef ONC_MAP_CAP
 #define ONC_MAP_CAP 512
 #define ONC_GSH_MIN 2
@@ -486,7 +494,10 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         const int64_t C0 = int64_t(S0 >> 4);
         const uint64_t B0 = uint64_t(C0) << 4;        // byte origin of the span-relative offsets
         if (lo_rec) wave_lds_sync();                   // the previous span's readers are done
-        for (int k = lane; k < kImgChunks; k += 64) T.img[k] = make_uint4(0, 0, 0, 0);   // records OR into it
+        // records OR into the image: zero the slots this span uses (the
+        // cut above bounds them by kImgChunks)
+        const int used = int(min(uint64_t(kImgChunks), lane_u64(wnp, hi_rec - 1) - wbase + 1));
+        for (int k = lane; k < used; k += 64) T.img[k] = make_uint4(0, 0, 0, 0);
         const bool active = lane >= lo_rec && lane < hi_rec;
         const int j = lane - lo_rec;
         const int64_t npx = active ? np : 0;

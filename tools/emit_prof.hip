@@ -3,7 +3,8 @@
 // Builds the product encode.hip with -DONC_EMIT_PROF: every tile records
 // s_memrealtime (100 MHz) at its phase boundaries (start, placement known,
 // plan + scan, span staged in LDS, span streamed, done). Runs enc_len +
-// enc_emit on a configs[1] batch (or configs[3] with argv[2] = "c3") and
+// enc_emit on a configs[1] batch (configs[3] with argv[2] = "c3", configs[0]'s
+// record shape with "c0") and
 // prints the mean / median duration of every phase per tile, the mean tile
 // lifetime and the mean number of tiles in flight.
 //
@@ -29,11 +30,16 @@
     } while (0)
 
 using namespace onc;
+namespace onc {
+thread_local LaunchEvents t_launch_events{nullptr, nullptr};   // defined by codec.hip in the library
+}
 
 int main(int argc, char** argv) {
     const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1000000;
-    const bool c3 = argc > 2 && std::string(argv[2]) == "c3";
-    const uint32_t P = c3 ? 1024 : 256;
+    // c3: AUTH_UNIX (16 gids) + 1 KiB; c0: the same credential + 64 B (configs[0]'s shape)
+    const bool c0 = argc > 2 && std::string(argv[2]) == "c0";
+    const bool c3 = c0 || (argc > 2 && std::string(argv[2]) == "c3");
+    const uint32_t P = c0 ? 64 : (c3 ? 1024 : 256);
     std::vector<onc_msg> msgs(n);
     std::vector<onc_unix_params> unix(c3 ? n : 1);
     const uint32_t gids[16] = {501, 12, 20, 61, 79, 80, 81, 98, 701, 33, 100, 204, 250, 395, 398, 399};
@@ -138,7 +144,7 @@ int main(int argc, char** argv) {
     for (double x : life) sum_life += x;
     const double span_us = double(t_max - t_min) * 10.0 / 1000.0;
     printf("%s: %llu records, %llu tiles; profiled enc_emit %.1f us (events); first tile start -> last tile end %.1f us\n",
-           c3 ? "configs[3]" : "configs[1]", (unsigned long long)n, (unsigned long long)tiles, best * 1000, span_us);
+           c0 ? "configs[0] shape" : (c3 ? "configs[3]" : "configs[1]"), (unsigned long long)n, (unsigned long long)tiles, best * 1000, span_us);
     printf("mean tile lifetime %.2f us; mean tiles in flight %.0f\n", sum_life / tiles, sum_life / span_us);
     for (int k = 0; k < 5; ++k) {
         std::sort(d[k].begin(), d[k].end());

@@ -19,6 +19,10 @@
         }                                                                                      \
     } while (0)
 
+namespace onc {
+thread_local LaunchEvents t_launch_events{nullptr, nullptr};   // defined by codec.hip in the library
+}
+
 static uint64_t sm(uint64_t& s) {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
