@@ -42,6 +42,7 @@ struct onc_codec {
 namespace onc {
 thread_local LaunchEvents t_launch_events{nullptr, nullptr};
 }
+constexpr uint64_t kWsMaxTiles = 32768;   // 2M records
 
 namespace {
 
@@ -330,8 +331,20 @@ int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
     bind_scratch(c, a);
     // Up to kFusedBlocks enc_len workgroups (1M records), enc_emit sums the
     // workgroup totals itself and the scan launch is skipped.
-    a.fused_base = onc::num_len_blocks(batch->n) <= onc::kFusedBlocks && !c->force_scan;
     a.variant = c->variant;
+    // enc_emit kernel choice: the wave-specialised kernel
+    // (a producer wave stages spans while three stream the previous one) for
+    // batches of <= 2M records whose payloads average >= 128 bytes — there
+    // it removes the lock-step staging rounds of the wave-per-tile kernel
+    // (configs[1]: enc_emit 123 -> 116 us); header-heavy records make its
+    // single producer the bottleneck (configs[0]-shaped: 117 -> 141 us) and
+    // at 8M records the wave-per-tile kernel's rounds are amortised (903 vs
+    // 945 us). Variant bits force it (0x200) or the wave-per-tile kernel
+    // (0x400). It places tiles from the workgroup totals itself at any size.
+    const uint64_t n = batch->n;
+    a.ws = (c->variant & 0x200) ||
+           (!(c->variant & 0x400) && n && onc::num_emit_tiles(n) <= kWsMaxTiles && batch->payload_len >= 128 * n);
+    a.fused_base = (onc::num_len_blocks(n) <= onc::kFusedBlocks && !c->force_scan) || a.ws;
     return ONC_RC_OK;
 }
 

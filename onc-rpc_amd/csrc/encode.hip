@@ -554,6 +554,344 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     ONC_PROF(5);
 }
 
+// ---------------------------------------------------------------------------
+// enc_emit, wave-specialised (ONC_EMIT_WS): a persistent workgroup of 4 waves
+// runs a two-slot pipeline over its tiles (tile = blockIdx.x + k * gridDim.x):
+// wave 0 (the producer) does everything enc_emit_tile does before the
+// stream — placement, plan, scans, the span's LDS image and maps — for the
+// next span into one slot while waves 1-3 (the consumers) stream the
+// previous span out of the other slot, interleaved by 1 KiB steps (consumer
+// c takes steps c, c + 3, ...). One workgroup barrier per span. The wave-
+// per-tile kernel keeps ~26 % of every tile's life in staging with no
+// memory traffic, and its tiles start in lock-step rounds, so those phases
+// coincide chip-wide; here the streams never stop for staging.
+struct SpanHdr {
+    uint64_t B0, S0, E;
+    int32_t NCe;
+    uint32_t gsh;
+    uint32_t byte_mode;
+    uint32_t state;          // 0: nothing to stream, 1: stream, 2: no more spans
+};
+struct WsSlot {
+    ImgTile T;
+    SpanHdr h;
+};
+
+// The producer's per-tile state: wave-uniform values in registers, the
+// per-record ones (lane = record) in LDS — kept in registers across the
+// phase loop they would be live in the consumers' stream too (178 VGPRs).
+struct WsTile {
+    uint64_t tile, r0;
+    int nrec, lo_rec;
+    bool byte_mode;
+    uint64_t run_blk, run_base;   // enc_len workgroup totals summed so far: [0, run_blk)
+};
+struct WsLane {
+    uint64_t len, poff, start, en, pst, wnp;
+    int64_t cfa, p0, p1, own_next;
+};
+
+// Tile placement without a scan launch and without the 16 pinned loads of
+// the fused wave-per-tile path: a workgroup's tiles ascend, so the producer
+// keeps a running sum of the enc_len workgroup totals and adds the ones
+// between its previous tile's workgroup and this one's (<= 64: one load
+// per lane), then the tile totals before the tile inside its workgroup.
+constexpr uint64_t kTilesPerBlk = kLenRecs / kEmitRecs;
+// A tile's prologue loads (its workgroup's tile totals, the workgroup totals
+// since the producer's previous tile, its descriptors), issued one tile
+// ahead: the producer's next tile is in flight across the barrier.
+struct WsLoads {
+    MsgRegs mr;
+    uint64_t tv, bw;
+};
+__device__ __forceinline__ WsLoads ws_issue(const EncArgs& a, uint64_t run_blk, uint64_t tile) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t t0 = tile / kTilesPerBlk * kTilesPerBlk;
+    const uint64_t r0 = tile * kEmitRecs;
+    const int nrec = int(min(uint64_t(kEmitRecs), a.n - r0));
+    WsLoads L;
+    L.tv = a.tile_sum[t0 + (uint64_t(lane) < kTilesPerBlk ? lane : 0)];
+    L.bw = a.block_sum[min(run_blk + lane, num_len_blocks(a.n) - 1)];
+    L.mr = issue_msg(a.msgs + r0 + min(lane, nrec - 1));
+    return L;
+}
+
+__device__ __forceinline__ void ws_begin_tile(const EncArgs& a, WsTile& S, WsLane* ln, uint64_t tile, WsLoads pf) {
+    const int lane = threadIdx.x & 63;
+    const uintptr_t payload = reinterpret_cast<uintptr_t>(a.payload_arena);
+    S.tile = tile;
+    S.r0 = tile * kEmitRecs;
+    S.nrec = int(min(uint64_t(kEmitRecs), a.n - S.r0));
+    S.lo_rec = 0;
+    const uint64_t blk = tile / kTilesPerBlk;
+    const uint64_t t0 = blk * kTilesPerBlk;
+    const uint64_t tv = pf.tv, bw = pf.bw;
+    const MsgRegs mr = pf.mr;
+    S.run_base += lane_u64(wave_incl_scan_u64(S.run_blk + lane < blk ? bw : 0), 63);
+    S.run_blk = blk;
+    const uint64_t T0 = a.origin + S.run_base + lane_u64(wave_incl_scan_u64(t0 + lane < tile ? tv : 0), 63);
+    const onc_msg dm = as_msg(mr);
+    uint64_t len = 0, poff = 0;
+    uint32_t hw = 0;
+    bool word_aligned = true;
+    if (lane < S.nrec) {
+        const RecPlan p = plan_record(dm, a.unix, a.bounds);
+        len = p.len;
+        hw = len ? meta_hw(p.meta) : 0;
+        poff = dm.payload_off;
+        word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((payload + dm.payload_off) & 3) == 0);
+    }
+    const uint64_t incl = wave_incl_scan_u64(len);
+    const uint64_t start = T0 + incl - len;
+    const uint64_t en = start + len;
+    const uint64_t pst = start + 4ull * hw;
+    if (lane < S.nrec) {
+        a.rec_off[S.r0 + lane] = start - a.origin;
+        if (S.r0 + lane + 1 == a.n) a.rec_off[a.n] = en - a.origin;
+        if (len != 0 && en > a.out_cap) a.status[S.r0 + lane] = ONC_ENC_WRITE_ZERO;
+    }
+    S.byte_mode = !(__all(word_aligned) && (T0 & 3) == 0);
+    const int64_t cfa = int64_t((start + 15) >> 4);
+    const int64_t p0 = int64_t((pst + 15) >> 4);
+    const int64_t p1 = max(p0, int64_t(en >> 4));
+    const int64_t np = len ? p1 - p0 : 0;
+    const int64_t cfa_next = int64_t(next_lane_u64(uint64_t(cfa)));
+    const int64_t cfa_end = int64_t((lane_u64(en, S.nrec - 1) + 15) >> 4);
+    const int64_t own_next = lane + 1 < S.nrec ? cfa_next : cfa_end;
+    const uint32_t nonpure = lane < S.nrec && len ? uint32_t(own_next - cfa - np) : 0u;
+    const uint64_t wnp = wave_incl_scan_u64(nonpure);
+    ln[lane] = WsLane{len, poff, start, en, pst, wnp, cfa, p0, p1, own_next};
+}
+
+// The next span of the producer's tile into slot W (image, entries, map,
+// header); advances S.lo_rec.
+__device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const WsLane* ln, WsSlot& W) {
+    const int lane = threadIdx.x & 63;
+    const WsLane L = ln[lane];
+    const uint64_t Slen = L.len, Spoff = L.poff, Sstart = L.start, Sen = L.en, Spst = L.pst, Swnp = L.wnp;
+    const int64_t Scfa = L.cfa, Sp0 = L.p0, Sp1 = L.p1, Sown_next = L.own_next;
+    const int64_t Snp = Slen ? Sp1 - Sp0 : 0;
+    const uint64_t Splen = Sen - Spst;
+    const uintptr_t payload = reinterpret_cast<uintptr_t>(a.payload_arena);
+    uint32_t* img32 = reinterpret_cast<uint32_t*>(W.T.img);
+    const int lo_rec = S.lo_rec, nrec = S.nrec;
+    const uint64_t wbase = lo_rec ? lane_u64(Swnp, lo_rec - 1) : 0;
+    const uint64_t sbeg = lane_u64(Sstart, lo_rec);
+    const uint64_t over = __ballot(lane > lo_rec && lane < nrec &&
+                                   (Swnp - wbase + 1 > uint64_t(kImgChunks) || Sen - sbeg > kSpanBytesMax));
+    const int hi_rec = over ? min(nrec, int(__builtin_ctzll(over))) : nrec;
+    const uint64_t S0 = sbeg;
+    const uint64_t S1 = lane_u64(Sen, hi_rec - 1);
+    const int64_t C0 = int64_t(S0 >> 4);
+    const uint64_t B0 = uint64_t(C0) << 4;
+    const int used = int(min(uint64_t(kImgChunks), lane_u64(Swnp, hi_rec - 1) - wbase + 1));
+    for (int k = lane; k < used; k += 64) W.T.img[k] = make_uint4(0, 0, 0, 0);
+    const bool active = lane >= lo_rec && lane < hi_rec;
+    const int j = lane - lo_rec;
+    const int64_t npx = active ? Snp : 0;
+    const int64_t NP = int64_t(wave_incl_scan_u64(uint64_t(npx))) - npx;
+    const int32_t NC = int32_t(((S1 + 15) >> 4) - C0);
+    uint32_t gsh = ONC_GSH_MIN;
+    while ((NC >> gsh) >= kMap2Cap) ++gsh;
+    const uint64_t nonempty = __ballot(active && Slen != 0);
+    wave_lds_sync();                                   // the zeroed image before the ORs
+    if (active) {
+        const bool small = Splen != 0 && Splen < 16;
+        const uintptr_t sb = payload + Spoff - Spst;
+        W.T.ent[j] = make_int4(int32_t(Scfa - C0), int32_t(Sp0 - C0), int32_t(Sp1 - C0), int32_t(NP));
+        const uint32_t ps = uint32_t(Spst - B0), pe = uint32_t(Sen - B0);
+        W.T.pay[j] = make_uint4(small ? pe : ps, pe, uint32_t(sb), uint32_t(sb >> 32));
+        if (Slen != 0) {
+            const uint64_t ibb = Sstart - 16ull * uint64_t(C0 + NP);
+            MsgRegs mr2 = issue_msg(a.msgs + S.r0 + lane);
+            asm volatile("" : "+v"(mr2.q[0]), "+v"(mr2.q[1]), "+v"(mr2.q[2]), "+v"(mr2.q[3]));
+            const onc_msg d = as_msg(mr2);
+            const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
+            ImgSink w{img32, uint32_t(ibb >> 2), 32u - 8u * uint32_t(ibb & 3), 0u};
+            put_header_words(d, uint32_t(Slen), src, w);
+            if (small) {
+                const uintptr_t pb = sb + Spst;
+                for (uint32_t k = 0; 4 * k < Splen; ++k) w(load4_masked(pb + 4 * k, pb + Splen));
+            }
+            w.finish();
+            const int32_t own_lo = (S0 & 15) && lane == __builtin_ctzll(nonempty) ? 0 : int32_t(Scfa - C0);
+            const int32_t own_hi = int32_t(Sown_next - C0);
+            const int32_t g_hi = min((own_hi + (1 << gsh) - 1) >> gsh, kMap2Cap);
+            for (int32_t g = (own_lo + (1 << gsh) - 1) >> gsh; g < g_hi; ++g) W.T.map[g] = uint8_t(j);
+        }
+    }
+    const uint64_t E = min(S1, a.out_cap);
+    if (lane == 0) {
+        W.T.ent[hi_rec - lo_rec] = make_int4(0x7FFFFFFF, 0, 0, 0);
+        SpanHdr h;
+        h.B0 = B0;
+        h.S0 = S0;
+        h.E = E;
+        h.NCe = E > S0 ? int32_t(((E + 15) >> 4) - C0) : 0;
+        h.gsh = gsh;
+        h.byte_mode = S.byte_mode ? 1u : 0u;
+        h.state = E > S0 ? 1u : 0u;
+        W.h = h;
+    }
+    S.lo_rec = hi_rec;
+}
+
+// stream_span for consumer `part` of `nparts`: the span's full chunks in
+// steps of 64 * kU chunks, this wave taking steps part, part + nparts, ...
+// (same two-register-set pipeline); part 0 also writes the partial edge
+// chunks.
+template <int kU, int kNT, bool kByte>
+__device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile& T, const SpanHdr& h, int part,
+                                                 int nparts, uintptr_t dummy) {
+    const int lane = threadIdx.x & 63;
+    constexpr int32_t S = 64 * kU;
+    const uint32_t gsh = h.gsh;
+    const uint64_t B0 = h.B0, S0 = h.S0, E = h.E;
+    const int32_t NCe = h.NCe;
+    const int32_t cf = S0 > B0 ? 1 : 0;
+    const int32_t cl = (E & 15) ? NCe - 1 : NCe;
+    const int32_t nsteps = cl > cf ? (cl - cf + S - 1) / S : 0;
+    if (part < nsteps) {
+        ChunkPlan Pa[kU], Pb[kU];
+        uint32_t Xa[kU][4], Xb[kU][4];
+        uint4 La[kU], Lb[kU];
+#define ONC_ISSUE(P, X, L, base)                                                          \
+    _Pragma("unroll") for (int u = 0; u < kU; ++u) {                                     \
+        P[u] = plan_chunk<kByte>(T, gsh, B0, min((base) + lane + 64 * u, cl - 1), dummy);   \
+        load_chunk<kNT, kByte>(P[u], X[u]);                                               \
+        L[u] = T.img[P[u].slot];                                                          \
+    }
+#define ONC_CONSUME(P, X, L, base)                                                        \
+    _Pragma("unroll") for (int u = 0; u < kU; ++u) {                                     \
+        const int32_t c = min((base) + lane + 64 * u, cl - 1);                            \
+        uint32_t v[4];                                                                    \
+        merge_chunk<kByte>(P[u], X[u], L[u], v);                                          \
+        u32x4* d = reinterpret_cast<u32x4*>(a.out + B0 + (uint64_t(c) << 4));             \
+        if (kNT & 2) __builtin_nontemporal_store(u32x4{v[0], v[1], v[2], v[3]}, d);        \
+        else *d = u32x4{v[0], v[1], v[2], v[3]};                                          \
+    }
+        int32_t jj = part;
+        ONC_ISSUE(Pa, Xa, La, cf + S * jj);
+        for (;;) {
+            ONC_ISSUE(Pb, Xb, Lb, cf + S * min(jj + nparts, nsteps - 1));
+            ONC_CONSUME(Pa, Xa, La, cf + S * jj);
+            jj += nparts;
+            if (jj >= nsteps) break;
+            ONC_ISSUE(Pa, Xa, La, cf + S * min(jj + nparts, nsteps - 1));
+            ONC_CONSUME(Pb, Xb, Lb, cf + S * jj);
+            jj += nparts;
+            if (jj >= nsteps) break;
+        }
+#undef ONC_ISSUE
+#undef ONC_CONSUME
+    }
+    if (part == 0) {
+        const bool e0 = lane == 0 && cf == 1;
+        const bool e1 = lane == 1 && cl == NCe - 1 && (NCe - 1 > 0 || cf == 0);
+        if (e0 || e1) {
+            const int32_t c = e0 ? 0 : NCe - 1;
+            const ChunkPlan P = plan_chunk<kByte>(T, gsh, B0, c, dummy);
+            uint32_t X[4];
+            load_chunk<kNT, kByte>(P, X);
+            const uint4 L = T.img[P.slot];
+            uint32_t v[4];
+            merge_chunk<kByte>(P, X, L, v);
+            const uint64_t o = B0 + (uint64_t(c) << 4);
+            store_chunk(a.out, o, max(o, S0), min(o + 16, E), v);
+        }
+    }
+}
+
+#ifndef ONC_WS_PREFETCH
+#define ONC_WS_PREFETCH 0     // the producer's next tile issued a phase ahead: measured no faster
+#endif
+#ifndef ONC_WS_U
+#define ONC_WS_U 2            // consumer chunks per lane per step (c1: 2 -> enc_emit 121 -> 116 us vs 1)
+#endif
+constexpr int kWsGrid = 1024;   // persistent workgroups (4 per CU on 256 CUs)
+static_assert(kWsGrid / kTilesPerBlk <= 64, "a producer adds at most 64 workgroup totals per tile");
+
+template <int kU, int kNT>
+__global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
+    __shared__ WsSlot s_slot[2];
+    __shared__ WsLane s_ln[64];
+    const int wv = threadIdx.x >> 6;
+    const uint64_t ntiles = num_emit_tiles(a.n);
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.msgs);
+    WsTile S;
+    S.run_blk = 0;
+    S.run_base = 0;
+    uint64_t next = blockIdx.x;
+    bool have = false;
+    WsLoads pf;
+    bool need_pf = false;
+    if (ONC_WS_PREFETCH && wv == 0 && next < ntiles) pf = ws_issue(a, 0, next);
+
+    // producer: one span into slot W, or "done"
+    const auto produce = [&](WsSlot& W) {
+        if (!have && next < ntiles) {
+            if (!ONC_WS_PREFETCH) pf = ws_issue(a, S.run_blk, next);
+            asm volatile("" : "+v"(pf.mr.q[0]), "+v"(pf.mr.q[1]), "+v"(pf.mr.q[2]), "+v"(pf.mr.q[3]), "+v"(pf.tv),
+                         "+v"(pf.bw));
+            ws_begin_tile(a, S, s_ln, next, pf);
+            next += gridDim.x;
+            have = true;
+            need_pf = next < ntiles;
+        }
+        if (!have) {
+            if ((threadIdx.x & 63) == 0) W.h.state = 2u;
+            return;
+        }
+        ws_stage_span(a, S, s_ln, W);
+        // issued after the span's own loads: one in-order vmcnt, so waiting
+        // for those must not wait for these
+        if (ONC_WS_PREFETCH && need_pf) pf = ws_issue(a, S.run_blk, next);
+        need_pf = false;
+        if (S.lo_rec >= S.nrec) have = false;
+    };
+#ifdef ONC_EMIT_PROF
+    uint64_t pr_t0 = wall_clock64(), pr_busy = 0, pr_phases = 0;
+#endif
+    if (wv == 0) produce(s_slot[0]);
+    __syncthreads();
+    int cur = 0;
+    for (;;) {
+        const uint32_t state = s_slot[cur].h.state;
+        if (state == 2u) break;
+#ifdef ONC_EMIT_PROF
+        const uint64_t pr_a = wall_clock64();
+#endif
+        if (wv == 0) {
+            produce(s_slot[cur ^ 1]);
+        } else if (state == 1u) {
+            const SpanHdr h = s_slot[cur].h;
+            if (h.byte_mode) stream_span_part<1, kNT, true>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
+            else stream_span_part<kU, kNT, false>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
+        }
+#ifdef ONC_EMIT_PROF
+        if (wv <= 1) {
+            __builtin_amdgcn_s_waitcnt(0);             // the wave's own memory operations done
+            pr_busy += wall_clock64() - pr_a;
+            ++pr_phases;
+        }
+#endif
+        __syncthreads();
+        cur ^= 1;
+    }
+#ifdef ONC_EMIT_PROF
+    // per workgroup: [0] lifetime, [1] producer busy, [2] phases, [4] consumer 1 busy
+    if (a.prof && (threadIdx.x & 63) == 0 && wv <= 1) {
+        if (wv == 0) {
+            a.prof[8 * blockIdx.x + 0] = wall_clock64() - pr_t0;
+            a.prof[8 * blockIdx.x + 1] = pr_busy;
+            a.prof[8 * blockIdx.x + 2] = pr_phases;
+        } else {
+            a.prof[8 * blockIdx.x + 4] = pr_busy;
+        }
+    }
+#endif
+}
+
 // kNT: bit 0 = nontemporal payload loads, bit 1 = nontemporal stores (a
 // measured alternative, header chunks stored temporally so that the decoder
 // finds them cached, made the decode slower: 60 -> 69 us on c1, the dirty
@@ -572,6 +910,11 @@ hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
+    if (a.ws) {
+        const uint32_t g = uint32_t(min(uint64_t(kWsGrid), num_emit_tiles(a.n)));
+        ONC_LAUNCH((enc_emit_ws_kernel<ONC_WS_U, kEmitNT>), dim3(g), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     const uint64_t blocks = (num_emit_tiles(a.n) + kFastWaves - 1) / kFastWaves;
     if (a.fused_base)
         ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, true>), dim3(uint32_t(blocks)),

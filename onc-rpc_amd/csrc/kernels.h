@@ -51,7 +51,8 @@ struct EncArgs {
     uint64_t* block_sum;    // enc_len workgroups (kLenRecs records): byte totals
     uint64_t* block_base;   // exclusive scan of block_sum (unused when fused_base)
     uint32_t fused_base;    // enc_emit sums block_sum itself (<= kFusedBlocks workgroups; no scan launch)
-    uint32_t variant;       // ONC_RPC_VARIANT bits (A/B experiments)
+    uint32_t variant;
+    uint32_t ws;            // enc_emit: the wave-specialised kernel (codec.hip enc_args decides)       // ONC_RPC_VARIANT bits (A/B experiments)
 #ifdef ONC_EMIT_PROF
     uint64_t* prof;         // lab builds only (tools/emit_prof.hip): per-tile phase timestamps
 #endif

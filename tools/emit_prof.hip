@@ -110,6 +110,8 @@ int main(int argc, char** argv) {
         fprintf(stderr, "n too large for the fused placement (lab keeps to <= 1M records)\n");
         return 1;
     }
+    const bool ws = argc > 3 && std::string(argv[3]) == "ws";   // the wave-specialised kernel
+    if (ws) a.ws = 1;
     a.prof = nullptr;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -129,6 +131,18 @@ int main(int argc, char** argv) {
     }
     std::vector<uint64_t> prof(tiles * 8);
     CK(hipMemcpy(prof.data(), d_prof, prof.size() * 8, hipMemcpyDeviceToHost));
+    if (ws) {
+        const uint64_t g = std::min<uint64_t>(1024, tiles);
+        double life = 0, pb = 0, cb = 0, ph = 0;
+        for (uint64_t w = 0; w < g; ++w) {
+            life += prof[8 * w] * 0.01; pb += prof[8 * w + 1] * 0.01; ph += prof[8 * w + 2]; cb += prof[8 * w + 4] * 0.01;
+        }
+        printf("wave-specialised: %llu workgroups, profiled enc_emit %.1f us; per workgroup: lifetime %.1f us, "
+               "%.1f phases, producer busy %.1f us (%.0f %%), consumer 1 busy %.1f us (%.0f %%), %.2f us per phase\n",
+               (unsigned long long)g, best * 1000, life / g, ph / g, pb / g, 100 * pb / life, cb / g, 100 * cb / life,
+               life / ph);
+        return 0;
+    }
     uint64_t t_min = ~0ull, t_max = 0;
     const char* names[5] = {"prologue loads (0->1)", "plan + scan (1->2)", "header build + map (2->3)",
                             "stream (3->4)", "tail (4->5)"};

@@ -107,6 +107,136 @@ static void clean_ceilings(const u32x4* scrub, uint64_t scrub16, uint32_t* sink)
     CK(hipFree(dst));
 }
 
+// Copy variants for the clean-state copy ceiling: a wave copies kK KiB
+// blocks (lane l: bytes 16l + 1024k, all kK loads issued before the first
+// store), blocks assigned by a grid-stride over the buffer; P = store policy,
+// LNT = nontemporal loads.
+template <int kK, int P, bool LNT>
+__global__ __launch_bounds__(256) void copy_blk_k(const u32x4* __restrict__ in, u32x4* __restrict__ out, uint64_t n16) {
+    const uint64_t waves = uint64_t(gridDim.x) * 4;
+    const int lane = threadIdx.x & 63;
+    for (uint64_t b = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); b * 64 * kK < n16; b += waves) {
+        const uint64_t o = b * 64 * kK + lane;
+        u32x4 v[kK];
+#pragma unroll
+        for (int k = 0; k < kK; ++k)
+            if (o + 64 * k < n16) v[k] = LNT ? __builtin_nontemporal_load(in + o + 64 * k) : in[o + 64 * k];
+#pragma unroll
+        for (int k = 0; k < kK; ++k)
+            if (o + 64 * k < n16) st16<P>(out + o + 64 * k, v[k]);
+    }
+}
+
+// Tile-structured copies (enc_emit's shape): a wave streams a contiguous
+// tile of kT KiB in 1 KiB steps, kD steps of loads in flight; or (kIL) the
+// 4 waves of a workgroup share a 4 x kT KiB tile, wave w taking steps
+// w, w + 4, ... so that the resident waves' accesses stay compact.
+template <int kT, int kD, bool kIL>
+__global__ __launch_bounds__(256) void copy_tile_k(const u32x4* __restrict__ in, u32x4* __restrict__ out, uint64_t n16) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t base, step;
+    if (kIL) { base = uint64_t(blockIdx.x) * 4 * kT * 64 + uint64_t(w) * 64; step = 4 * 64; }
+    else { base = (uint64_t(blockIdx.x) * 4 + w) * kT * 64; step = 64; }
+    u32x4 v[kD];
+#pragma unroll
+    for (int d = 0; d < kD; ++d) {
+        const uint64_t o = base + d * step + lane;
+        if (o < n16) v[d] = in[o];
+    }
+    for (int s = 0; s < kT; s += kD) {
+#pragma unroll
+        for (int d = 0; d < kD; ++d) {
+            const uint64_t o = base + uint64_t(s + d) * step + lane;
+            const uint64_t on = base + uint64_t(s + d + kD) * step + lane;
+            const u32x4 x = v[d];
+            if (s + d + kD < kT && on < n16) v[d] = in[on];
+            if (s + d < kT && o < n16) __builtin_nontemporal_store(x, out + o);
+        }
+    }
+}
+
+// Channel-camping probe: tiles of kT KiB at a stride of kT KiB, a wave
+// streaming its tile in 1 KiB steps (1 in flight); kRot: the wave starts at
+// step (tile mod kT) and wraps, so waves at the same moment touch different
+// offsets of their tiles.
+template <int kT, bool kRot>
+__global__ __launch_bounds__(256) void copy_tile_rot_k(const u32x4* __restrict__ in, u32x4* __restrict__ out,
+                                                       uint64_t n16) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t tile = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    const uint64_t base = tile * kT * 64;
+    const int rot = kRot ? int(tile % kT) : 0;
+    for (int s = 0; s < kT; ++s) {
+        int j = s + rot;
+        if (j >= kT) j -= kT;
+        const uint64_t o = base + uint64_t(j) * 64 + lane;
+        if (o < n16) __builtin_nontemporal_store(in[o], out + o);
+    }
+}
+
+static void copy_variants(const u32x4* scrub, uint64_t scrub16, uint32_t* sink) {
+    const size_t wb = size_t(300) * 1000 * 1000;
+    void *src, *dst;
+    CK(hipMalloc(&src, wb));
+    CK(hipMalloc(&dst, wb));
+    CK(hipMemset(src, 3, wb));
+    CK(hipMemset(dst, 0, wb));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    struct V { const char* name; void (*f)(const u32x4*, u32x4*, uint64_t); int grid; };
+    const V vs[] = {
+        {"blk 2 KiB/wave, nt st, grid 2048", copy_blk_k<2, 1, false>, 2048},
+        {"blk 4 KiB/wave, nt st, grid 2048", copy_blk_k<4, 1, false>, 2048},
+        {"blk 4 KiB/wave, nt st, grid 1024", copy_blk_k<4, 1, false>, 1024},
+        {"blk 8 KiB/wave, nt st, grid 1024", copy_blk_k<8, 1, false>, 1024},
+        {"blk 4 KiB/wave, nt ld+st, grid 2048", copy_blk_k<4, 1, true>, 2048},
+        {"blk 4 KiB/wave, sc0 sc1 nt st, g 2048", copy_blk_k<4, 5, false>, 2048},
+        {"blk 4 KiB/wave, plain st, grid 2048", copy_blk_k<4, 0, false>, 2048},
+        {"blk 4 KiB/wave, nt st, one pass", copy_blk_k<4, 1, false>, int((wb / 16 / 256 + 3) / 4)},
+        {"blk 1 KiB/wave, nt st, one pass", copy_blk_k<1, 1, false>, int((wb / 16 / 64 + 3) / 4)},
+        {"tile 16 KiB/wave, 1 step in flight", copy_tile_k<16, 1, false>, int((wb / 16 / 1024 + 3) / 4)},
+        {"tile 16 KiB/wave, 2 steps in flight", copy_tile_k<16, 2, false>, int((wb / 16 / 1024 + 3) / 4)},
+        {"tile 4 KiB/wave, 2 steps in flight", copy_tile_k<4, 2, false>, int((wb / 16 / 256 + 3) / 4)},
+        {"tile 64 KiB/WG interleaved, 2 in flight", copy_tile_k<16, 2, true>, int((wb / 16 / 1024 + 3) / 4)},
+        {"tile 16 KiB/WG interleaved, 2 in flight", copy_tile_k<4, 2, true>, int((wb / 16 / 256 + 3) / 4)},
+        {"blk 2 KiB/wave, nt st, one pass", copy_blk_k<2, 1, false>, int((wb / 16 / 128 + 3) / 4)},
+        {"blk 1 KiB/wave, nt st, grid 2048", copy_blk_k<1, 1, false>, 2048},
+        {"blk 1 KiB/wave, nt st, grid 8192", copy_blk_k<1, 1, false>, 8192},
+        {"tile 4 KiB/wave, 1 step in flight", copy_tile_k<4, 1, false>, int((wb / 16 / 256 + 3) / 4)},
+        {"tile 2 KiB/wave, 1 step in flight", copy_tile_k<2, 1, false>, int((wb / 16 / 128 + 3) / 4)},
+        {"tile 8 KiB/wave, 2 steps in flight", copy_tile_k<8, 2, false>, int((wb / 16 / 512 + 3) / 4)},
+        {"camp: tile 16 KiB, in order", copy_tile_rot_k<16, false>, int((wb / 16 / 1024 + 3) / 4)},
+        {"camp: tile 16 KiB, rotated start", copy_tile_rot_k<16, true>, int((wb / 16 / 1024 + 3) / 4)},
+        {"camp: tile 18 KiB, in order", copy_tile_rot_k<18, false>, int((wb / 16 / 1152 + 3) / 4)},
+        {"camp: tile 19 KiB, in order", copy_tile_rot_k<19, false>, int((wb / 16 / 1216 + 3) / 4)},
+        {"camp: tile 19 KiB, rotated start", copy_tile_rot_k<19, true>, int((wb / 16 / 1216 + 3) / 4)},
+    };
+    const int nv = sizeof(vs) / sizeof(vs[0]);
+    std::vector<float> t[32];
+    for (int rep = 0; rep < 10; ++rep) {
+        for (int k = 0; k < nv; ++k) {
+            hipLaunchKernelGGL(read_k, dim3(8192), dim3(256), 0, 0, scrub, scrub16, sink);
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, 0));
+            hipLaunchKernelGGL(vs[k].f, dim3(vs[k].grid), dim3(256), 0, 0, (const u32x4*)src, (u32x4*)dst, wb / 16);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (rep >= 2) t[k].push_back(ms * 1000.f);
+        }
+    }
+    printf("clean-state copies of 300 MB (read 300 + write 300):\n");
+    for (int k = 0; k < nv; ++k) {
+        std::sort(t[k].begin(), t[k].end());
+        const float m = t[k][t[k].size() / 2];
+        printf("  %-40s %8.1f us  %6.2f TB/s\n", vs[k].name, m, 2.0 * wb / (m * 1e-6) / 1e12);
+    }
+    CK(hipFree(src));
+    CK(hipFree(dst));
+}
+
 int main() {
     const size_t nb = size_t(256) << 20, ob = size_t(320) << 20;
     void *src, *dst, *other;
@@ -166,5 +296,6 @@ int main() {
     CK(hipMalloc(&scrub, sb));
     CK(hipMemset(scrub, 7, sb));
     clean_ceilings((const u32x4*)scrub, sb / 16, sink);
+    copy_variants((const u32x4*)scrub, sb / 16, sink);
     return 0;
 }
