@@ -808,6 +808,9 @@ __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile
 #ifndef ONC_WS_U
 #define ONC_WS_U 2            // consumer chunks per lane per step (c1: 2 -> enc_emit 121 -> 116 us vs 1)
 #endif
+#ifndef ONC_WS_EVEN
+#define ONC_WS_EVEN 0   // 1: trim the grid to equal tiles per workgroup (977 for configs[1]): measured slower
+#endif
 constexpr int kWsGrid = 1024;   // persistent workgroups (4 per CU on 256 CUs)
 static_assert(kWsGrid / kTilesPerBlk <= 64, "a producer adds at most 64 workgroup totals per tile");
 
@@ -911,7 +914,9 @@ hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
 
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
     if (a.ws) {
-        const uint32_t g = uint32_t(min(uint64_t(kWsGrid), num_emit_tiles(a.n)));
+        const uint64_t tiles = num_emit_tiles(a.n);
+        const uint64_t per = (tiles + kWsGrid - 1) / kWsGrid;
+        const uint32_t g = uint32_t(ONC_WS_EVEN ? (tiles + per - 1) / per : min(uint64_t(kWsGrid), tiles));
         ONC_LAUNCH((enc_emit_ws_kernel<ONC_WS_U, kEmitNT>), dim3(g), dim3(256), 0, s, a);
         return hipGetLastError();
     }
