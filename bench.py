@@ -555,6 +555,9 @@ def roofline(tm, n, sum_W, sum_H, step_alg, ms_per_step, traffic, traffic_src):
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
             "alg_bytes_per_launch": alg, "avg_launch_us": dom_us, "launches_timed": dom_cnt,
             "timed_every_nth_step": tm.stride,
+            **({"kernel_note": "ONC_K_ENC_EMIT launch: the wave-specialised enc_emit_ws_kernel for batches of "
+                               "<= 2M records with >= 128 B mean payload, else enc_emit_kernel_t (codec.hip "
+                               "enc_args)"} if tm.dom == "enc_emit_kernel" else {}),
             # the whole step (every kernel of the metric), per GPU
             "step_alg_bytes": step_alg, "step_achieved": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS}
 
