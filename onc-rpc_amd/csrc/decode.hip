@@ -33,20 +33,24 @@ namespace onc {
 constexpr uint32_t kWin1 = ONC_DEC_WIN < 4 ? ONC_DEC_WIN : 4;
 constexpr uint32_t kWinChunks = ONC_DEC_WIN;
 constexpr uint32_t kWinWords = 4 * kWinChunks;
+#ifndef ONC_DEC_TILE
+#define ONC_DEC_TILE 64     // c1 decode 54.7 -> 50.2 us, c2 81 -> 78.6, c3 447 -> 468 vs 256 (profiles/lab_r02_dec_tile.log)
+#endif
+constexpr int kDecTile = ONC_DEC_TILE;        // records (lanes) per decode workgroup
 
 struct Rd {
     uintptr_t base;          // absolute address of record byte 0
     uint32_t q0;             // window offset of record byte 0 (0..15)
     uint32_t lim;            // window bytes loaded
-    const uint32_t* col;     // this lane's window column (stride kTile words)
+    const uint32_t* col;     // this lane's window column (stride kDecTile words)
 
     // Big-endian u32 at record-relative position pos (all 4 bytes valid).
     __device__ __forceinline__ uint32_t be32(uint32_t pos) const {
         const uint32_t q = q0 + pos;
         if (q + 4u <= lim) {
             const uint32_t wi = q >> 2, sh = q & 3u;
-            const uint32_t w0 = col[wi * kTile];
-            const uint32_t w1 = sh ? col[(wi + 1) * kTile] : 0u;
+            const uint32_t w0 = col[wi * kDecTile];
+            const uint32_t w1 = sh ? col[(wi + 1) * kDecTile] : 0u;
             return bswap(funnel(w0, w1, sh));
         }
         return bswap(load4(base + pos));
@@ -332,11 +336,11 @@ __device__ __forceinline__ int32_t parse_record(const Rd& R, uint64_t L, uint64_
 // apart, cold: 53 / 59 / 65 / 71 us — ~53 us per million lines). Measured
 // c1 decode 59.6 -> 56.0 us, c2 90.1 -> 88.5 us, c3 unchanged.
 template <int MODE, bool kExact = false, bool kNTOut = false>
-__global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
-    __shared__ uint32_t s_win[kWinWords * kTile];
-    static_assert(kWinWords * kTile * 4 >= kTile * sizeof(onc_msg), "descriptor staging reuses the window");
+__global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
+    __shared__ uint32_t s_win[kWinWords * kDecTile];
+    static_assert(kWinWords * kDecTile * 4 >= kDecTile * sizeof(onc_msg), "descriptor staging reuses the window");
     const int t = threadIdx.x;
-    const uint64_t i0 = uint64_t(blockIdx.x) * kTile;
+    const uint64_t i0 = uint64_t(blockIdx.x) * kDecTile;
     const uint64_t i = i0 + t;
     const bool valid = i < a.n;
     uint64_t b = 0, L = 0;
@@ -362,10 +366,10 @@ __global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
 #pragma unroll
         for (uint32_t j = 0; j < kWin1; ++j) {
             if (j < nch) {
-                s_win[(4 * j + 0) * kTile + t] = v[j].x;
-                s_win[(4 * j + 1) * kTile + t] = v[j].y;
-                s_win[(4 * j + 2) * kTile + t] = v[j].z;
-                s_win[(4 * j + 3) * kTile + t] = v[j].w;
+                s_win[(4 * j + 0) * kDecTile + t] = v[j].x;
+                s_win[(4 * j + 1) * kDecTile + t] = v[j].y;
+                s_win[(4 * j + 2) * kDecTile + t] = v[j].z;
+                s_win[(4 * j + 3) * kDecTile + t] = v[j].w;
             }
         }
         // Header extent from the first round: call -> 36 + cred body + verf
@@ -404,10 +408,10 @@ __global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
 #pragma unroll
             for (uint32_t j = kR2; j < kWinChunks; ++j) {
                 if (j >= nch && j < want) {
-                    s_win[(4 * j + 0) * kTile + t] = w[j - kR2].x;
-                    s_win[(4 * j + 1) * kTile + t] = w[j - kR2].y;
-                    s_win[(4 * j + 2) * kTile + t] = w[j - kR2].z;
-                    s_win[(4 * j + 3) * kTile + t] = w[j - kR2].w;
+                    s_win[(4 * j + 0) * kDecTile + t] = w[j - kR2].x;
+                    s_win[(4 * j + 1) * kDecTile + t] = w[j - kR2].y;
+                    s_win[(4 * j + 2) * kDecTile + t] = w[j - kR2].z;
+                    s_win[(4 * j + 3) * kDecTile + t] = w[j - kR2].w;
                 }
             }
             nch = want;
@@ -441,11 +445,11 @@ __global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) stage[4 * t + k] = mz[k];
     __syncthreads();
-    const uint64_t nblk = min(uint64_t(kTile), a.n - i0);
+    const uint64_t nblk = min(uint64_t(kDecTile), a.n - i0);
     uint4* dst = reinterpret_cast<uint4*>(a.out.msgs + i0);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const uint32_t j = uint32_t(k * kTile + t);
+        const uint32_t j = uint32_t(k * kDecTile + t);
         if (j < 4 * nblk) {
             if (kNTOut) {
                 const uint4 v = stage[j];
@@ -457,11 +461,11 @@ __global__ __launch_bounds__(kTile) void decode_kernel(DecArgs a) {
 }
 
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s) {
-    const uint64_t tiles = num_tiles(a.n);
+    const uint64_t tiles = (a.n + kDecTile - 1) / kDecTile;
     if (mode == ONC_DECODE_BYTES)
-        ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true>), dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
+        ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true>), dim3(uint32_t(tiles)), dim3(kDecTile), 0, s, a);
     else
-        ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true>), dim3(uint32_t(tiles)), dim3(kTile), 0, s, a);
+        ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true>), dim3(uint32_t(tiles)), dim3(kDecTile), 0, s, a);
     return hipGetLastError();
 }
 
