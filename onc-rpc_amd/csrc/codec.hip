@@ -334,7 +334,9 @@ int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
     a.variant = c->variant;
     // enc_emit kernel choice: the wave-specialised kernel
     // (a producer wave stages spans while three stream the previous one) for
-    // batches of <= 2M records whose payloads average >= 128 bytes — there
+    // batches of <= 2M records whose payloads average >= 128 bytes (or of
+    // any size when they average >= 512 bytes: configs[3], 4M x 1 KiB,
+    // enc_emit 1808 -> 1765 us) — there
     // it removes the lock-step staging rounds of the wave-per-tile kernel
     // (configs[1]: enc_emit 123 -> 116 us); header-heavy records make its
     // single producer the bottleneck (configs[0]-shaped: 117 -> 141 us) and
@@ -342,8 +344,11 @@ int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
     // 945 us). Variant bits force it (0x200) or the wave-per-tile kernel
     // (0x400). It places tiles from the workgroup totals itself at any size.
     const uint64_t n = batch->n;
-    a.ws = (c->variant & 0x200) ||
-           (!(c->variant & 0x400) && n && onc::num_emit_tiles(n) <= kWsMaxTiles && batch->payload_len >= 128 * n);
+    // a.ws: 0 wave-per-tile; 1 wave-specialised, 2 KiB consumer steps; 2 the
+    // same with 1 KiB steps (long payloads: configs[3] 1770 vs 1815 us)
+    const bool big = batch->payload_len >= 512 * n;
+    const bool ws_shape = batch->payload_len >= 128 * n && (onc::num_emit_tiles(n) <= kWsMaxTiles || big);
+    a.ws = ((c->variant & 0x200) || (!(c->variant & 0x400) && n && ws_shape)) ? (big ? 2u : 1u) : 0u;
     a.fused_base = (onc::num_len_blocks(n) <= onc::kFusedBlocks && !c->force_scan) || a.ws;
     return ONC_RC_OK;
 }

@@ -917,7 +917,8 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
         const uint64_t tiles = num_emit_tiles(a.n);
         const uint64_t per = (tiles + kWsGrid - 1) / kWsGrid;
         const uint32_t g = uint32_t(ONC_WS_EVEN ? (tiles + per - 1) / per : min(uint64_t(kWsGrid), tiles));
-        ONC_LAUNCH((enc_emit_ws_kernel<ONC_WS_U, kEmitNT>), dim3(g), dim3(256), 0, s, a);
+        if (a.ws == 2) ONC_LAUNCH((enc_emit_ws_kernel<1, kEmitNT>), dim3(g), dim3(256), 0, s, a);
+        else ONC_LAUNCH((enc_emit_ws_kernel<ONC_WS_U, kEmitNT>), dim3(g), dim3(256), 0, s, a);
         return hipGetLastError();
     }
     const uint64_t blocks = (num_emit_tiles(a.n) + kFastWaves - 1) / kFastWaves;

@@ -74,7 +74,7 @@ def test_call_none_many_tiles(codec, R, oracle, shift):
     _check(R, codec, oracle, S.call_none(200_000, 256, seed=31), shift)
 
 
-@pytest.mark.parametrize("gen", ["mixed", "random", "unix16", "odd"])
+@pytest.mark.parametrize("gen", ["mixed", "random", "unix16", "odd", "big", "big_odd"])
 def test_shapes(codec, R, oracle, gen):
     if gen == "mixed":
         hb = S.mixed(40_000, seed=32, pmin=0, pmax=900, exotic=0.1)
@@ -82,8 +82,12 @@ def test_shapes(codec, R, oracle, gen):
         hb = L.build_batch(S.random_messages(20_000, seed=33, max_payload=700))
     elif gen == "unix16":
         hb = S.call_unix16(30_000, 64, seed=34)
-    else:
+    elif gen == "odd":
         hb = S.call_none(50_000, 257, seed=35)       # odd payloads: the byte path in every tile
+    elif gen == "big":
+        hb = S.call_unix16(20_000, 1024, seed=39)    # >= 512 B mean payload: 1 KiB consumer steps
+    else:
+        hb = S.call_none(20_000, 1023, seed=40)
     _check(R, codec, oracle, hb)
     _check(R, codec, oracle, hb, shift=11)
 
