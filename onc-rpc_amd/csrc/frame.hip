@@ -61,10 +61,14 @@ struct GlobalStarts {       // straight to the chunk's slice of a.starts (the wa
         if (rec) rec[i] = p;
     }
 };
-struct LdsStarts {          // chunk-relative u32 in an LDS column (stride 256), copied out after the chase:
+#ifndef ONC_FRAME_CHUNKS_WG
+#define ONC_FRAME_CHUNKS_WG 64   // 512 waves spread over every CU: c2 framing chase 37.0 -> 34.6 us vs 256
+#endif
+constexpr int kChunksWG = ONC_FRAME_CHUNKS_WG;   // lanes (chunks) per frame_chunks workgroup
+struct LdsStarts {          // chunk-relative u32 in an LDS column (stride kChunksWG), copied out after the chase:
     uint32_t* col;          // a global store inside the chase would hold up the next hop's load (one vmcnt)
     uint64_t c0;
-    __device__ __forceinline__ void operator()(uint32_t i, uint64_t p) const { col[i * 256] = uint32_t(p - c0); }
+    __device__ __forceinline__ void operator()(uint32_t i, uint64_t p) const { col[i * kChunksWG] = uint32_t(p - c0); }
 };
 template <class Sink>
 __device__ __forceinline__ Chase chase(const FrameArgs& a, uint64_t p, uint64_t lim, const Sink& rec) {
@@ -259,8 +263,8 @@ __device__ __forceinline__ void put_chase(const FrameArgs& a, uint64_t t, const 
     a.aux[2 * t + 1] = c.aux1;
 }
 
-__global__ __launch_bounds__(256) void frame_chunks_kernel(FrameArgs a) {
-    __shared__ uint32_t s_rec[kStartsCap * 256];
+__global__ __launch_bounds__(kChunksWG) void frame_chunks_kernel(FrameArgs a) {
+    __shared__ uint32_t s_rec[kStartsCap * kChunksWG];
     const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (t == 0) {
         *a.first_fail = kNone;
@@ -279,7 +283,7 @@ __global__ __launch_bounds__(256) void frame_chunks_kernel(FrameArgs a) {
     const Chase c = chase(a, g, c1, LdsStarts{&s_rec[threadIdx.x], c0});
     put_chase(a, t, c);
     uint64_t* rec = a.starts + t * kStartsCap;
-    for (uint32_t i = 0; i < min(c.cnt, kStartsCap); ++i) rec[i] = c0 + s_rec[i * 256 + threadIdx.x];
+    for (uint32_t i = 0; i < min(c.cnt, kStartsCap); ++i) rec[i] = c0 + s_rec[i * kChunksWG + threadIdx.x];
 }
 
 // fail[t] = 1 when guessed chunk t's chain does not land on a guess, or jumps
@@ -546,8 +550,8 @@ hipError_t launch_frame_guess(const FrameArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_frame_chunks(const FrameArgs& a, hipStream_t s) {
-    const uint32_t blocks = uint32_t((a.nchunks + 255) / 256);
-    ONC_LAUNCH(frame_chunks_kernel, dim3(blocks), dim3(256), 0, s, a);
+    const uint32_t blocks = uint32_t((a.nchunks + kChunksWG - 1) / kChunksWG);
+    ONC_LAUNCH(frame_chunks_kernel, dim3(blocks), dim3(kChunksWG), 0, s, a);
     return hipGetLastError();
 }
 
