@@ -443,7 +443,7 @@ ALG_PER_LAUNCH = {
     "iov_emit_kernel": lambda n, W, H: 0,
     "frame_chunks_kernel": lambda n, W, H: 0,
     "frame_write_kernel": lambda n, W, H: 8 * n,
-    "frame_verify_kernel": lambda n, W, H: 0,
+    "frame_coff_kernel": lambda n, W, H: 0,
     "frame_walk_kernel": lambda n, W, H: 0,
     "frame_counts_kernel": lambda n, W, H: 0,
     "frame_guess_kernel": lambda n, W, H: 0,

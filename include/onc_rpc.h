@@ -41,8 +41,10 @@ extern "C" {
 #endif
 
 /* 2: onc_batch carries arena sizes (bounds-checked descriptors), onc_encode
- *    accepts any output address, retired kernel id ONC_K_ENC_FIXUP removed. */
-#define ONC_RPC_ABI_VERSION 2
+ *    accepts any output address, retired kernel id ONC_K_ENC_FIXUP removed.
+ * 3: timing id 10 is ONC_K_FRAME_OFFSETS (the framer's chunk verification
+ *    now runs inside frame_chunks; ONC_K_FRAME_VERIFY is gone). */
+#define ONC_RPC_ABI_VERSION 3
 
 /* ------------------------------------------------------------------------ */
 /* Wire discriminants (values are the on-wire u32s)                          */
@@ -255,10 +257,16 @@ int onc_abi_version(void);
 
 /* Per-kernel event timing (for the bench's roofline). `enable` is a bitmask
  * of kernel ids (1 << ONC_K_*; ONC_TIMING_ALL = every kernel, 0 = off): each
- * launch of a selected kernel is bracketed by hipEvents on the codec
- * stream; the accumulated device time and launch count per kernel id are
- * returned by onc_codec_kernel_stats after a sync. Timing only the kernel
- * of interest keeps the event overhead off the other launches. */
+ * launch of a selected kernel carries start/stop hipEvents on the codec
+ * stream (hipExtLaunchKernelGGL: the dispatch's own timestamps); the
+ * accumulated device time and launch count per kernel id are returned by
+ * onc_codec_kernel_stats after a sync. Timing only the kernel of interest
+ * keeps the event overhead off the other launches. An id names a launch
+ * site: ONC_K_ENC_EMIT is either enc_emit kernel; ONC_K_LEN_TILES /
+ * ONC_K_LEN_APPLY are onc_scan_lengths' first and second launch (lenblk /
+ * lenoff up to 8M records); ONC_K_FRAME_COUNTS / ONC_K_FRAME_OFFSETS the
+ * framer's count scan (frame_cblk / frame_coff, or frame_counts and the
+ * three-launch scan beyond 512k chunks). */
 #define ONC_K_ENC_LEN      0
 #define ONC_K_SCAN_TILES   1
 #define ONC_K_ENC_EMIT     2
@@ -269,7 +277,7 @@ int onc_abi_version(void);
 #define ONC_K_IOV_EMIT     7
 #define ONC_K_FRAME        8
 #define ONC_K_FRAME_WRITE  9
-#define ONC_K_FRAME_VERIFY 10
+#define ONC_K_FRAME_OFFSETS 10
 #define ONC_K_FRAME_WALK   11
 #define ONC_K_FRAME_COUNTS 12
 #define ONC_K_FRAME_GUESS  13

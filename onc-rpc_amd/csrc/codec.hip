@@ -232,7 +232,7 @@ const char* onc_kernel_name(int k) {
         case ONC_K_IOV_EMIT: return "iov_emit_kernel";
         case ONC_K_FRAME: return "frame_chunks_kernel";
         case ONC_K_FRAME_WRITE: return "frame_write_kernel";
-        case ONC_K_FRAME_VERIFY: return "frame_verify_kernel";
+        case ONC_K_FRAME_OFFSETS: return "frame_coff_kernel";
         case ONC_K_FRAME_WALK: return "frame_walk_kernel";
         case ONC_K_FRAME_COUNTS: return "frame_counts_kernel";
         case ONC_K_FRAME_GUESS: return "frame_guess_kernel";
@@ -540,8 +540,6 @@ int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* 
     if (rc != ONC_RC_OK) return rc;
     rc = run(c, ONC_K_FRAME, "frame_chunks", [&] { return onc::launch_frame_chunks(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
-    rc = run(c, ONC_K_FRAME_VERIFY, "frame_verify", [&] { return onc::launch_frame_verify(a, c->stream); });
-    if (rc != ONC_RC_OK) return rc;
     rc = run(c, ONC_K_FRAME_WALK, "frame_walk", [&] { return onc::launch_frame_walk(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
     if (onc::frame_fused_scan_ok(P) && !c->force_scan) {
@@ -549,7 +547,7 @@ int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* 
         // chunk copying its kept record starts
         rc = run(c, ONC_K_FRAME_COUNTS, "frame_cblk", [&] { return onc::launch_frame_cblk(a, tile_sum, c->stream); });
         if (rc != ONC_RC_OK) return rc;
-        rc = run(c, ONC_K_LEN_APPLY, "frame_coff", [&] { return onc::launch_frame_coff(a, tile_sum, c->stream); });
+        rc = run(c, ONC_K_FRAME_OFFSETS, "frame_coff", [&] { return onc::launch_frame_coff(a, tile_sum, c->stream); });
         if (rc != ONC_RC_OK) return rc;
         return run(c, ONC_K_FRAME_WRITE, "frame_write", [&] { return onc::launch_frame_write_slots(a, c->stream); });
     }

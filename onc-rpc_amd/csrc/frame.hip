@@ -17,11 +17,11 @@
 //                 (header length only, as the reference does) out of the
 //                 chunk: exit position and record count, or where and why
 //                 the chain stops.
-//   frame_verify  lane per chunk: a guessed chunk is consistent when its
-//                 chain lands exactly on the guess of the chunk it lands in
-//                 and every chunk it jumps over has no guess. Because chunk 0
-//                 is exact, every guessed chunk before the first
-//                 inconsistency is on the true chain (induction).
+//                 Then (same lane) the check: a guessed chunk is consistent
+//                 when its chain lands exactly on the guess of the chunk it
+//                 lands in and every chunk it jumps over has no guess.
+//                 Because chunk 0 is exact, every guessed chunk before the
+//                 first inconsistency is on the true chain (induction).
 //   frame_walk    one wave, only when a check failed (payload bytes that
 //                 look like headers, or records that do not look like
 //                 RPC messages): walks the true chain from the first
@@ -165,6 +165,15 @@ constexpr int kGuessWin = 272;            // dwords per staged step: 1 KiB + 64 
 __global__ __launch_bounds__(256) void frame_guess_kernel(FrameArgs a) {
     __shared__ uint32_t s_win[4][kGuessSub][kGuessWin];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    {   // the verification flags of frame_chunks (set there, read by the walk)
+        const uint64_t f = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+        if (f == 0) {
+            *a.first_fail = kNone;
+            *a.first_stop = kNone;
+        }
+        if (f < ((a.nchunks + 255) >> 8)) a.fail2[f] = a.stop2[f] = 0;
+        if (f < ((a.nchunks + 65535) >> 16)) a.fail3[f] = a.stop3[f] = 0;
+    }
     const uint64_t t0 = (uint64_t(blockIdx.x) * 4 + wv) * kGuessSub;
     if (t0 >= a.nchunks) return;
     const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire);
@@ -263,49 +272,38 @@ __device__ __forceinline__ void put_chase(const FrameArgs& a, uint64_t t, const 
     a.aux[2 * t + 1] = c.aux1;
 }
 
+// frame_chunks: lane per chunk, the exact chain from the guess out of the
+// chunk, then the chunk's verification: fail[t] = 1 when guessed chunk t's
+// chain does not land on a guess, or jumps over a guessed chunk; stop[t] = 1
+// when its chain ends in it. Both also set their per-256-chunk and
+// per-65536-chunk summary flags (zeroed by frame_guess) so that the walk
+// finds the next set flag in three short ballot scans; first_fail /
+// first_stop = the minimum flagged chunk. (The check reads only the guesses,
+// final before this launch, and the lane's own chase: one launch fewer than
+// a separate verification pass.)
 __global__ __launch_bounds__(kChunksWG) void frame_chunks_kernel(FrameArgs a) {
     __shared__ uint32_t s_rec[kStartsCap * kChunksWG];
     const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (t == 0) {
-        *a.first_fail = kNone;
-        *a.first_stop = kNone;
-    }
-    if (t < ((a.nchunks + 255) >> 8)) a.fail2[t] = a.stop2[t] = 0;
-    if (t < ((a.nchunks + 65535) >> 16)) a.fail3[t] = a.stop3[t] = 0;
     if (t >= a.nchunks) return;
     const uint64_t c0 = t * a.chunk;
     const uint64_t c1 = min(c0 + a.chunk, a.len);
     const uint64_t g = a.g[t];                 // frame_guess
+    uint8_t bad = 0, stop = 0;
     if (g == kNone) {
         put_chase(a, t, Chase{kNone, 0, kExit, 0, 0});
-        return;
-    }
-    const Chase c = chase(a, g, c1, LdsStarts{&s_rec[threadIdx.x], c0});
-    put_chase(a, t, c);
-    uint64_t* rec = a.starts + t * kStartsCap;
-    for (uint32_t i = 0; i < min(c.cnt, kStartsCap); ++i) rec[i] = c0 + s_rec[i * kChunksWG + threadIdx.x];
-}
-
-// fail[t] = 1 when guessed chunk t's chain does not land on a guess, or jumps
-// over a guessed chunk; stop[t] = 1 when guessed chunk t's chain ends there.
-// Both also set their per-256-chunk and per-65536-chunk summary flags (zeroed
-// by frame_chunks) so that the walk finds the next set flag in three short
-// ballot scans; first_fail / first_stop = the minimum flagged chunk.
-__global__ __launch_bounds__(256) void frame_verify_kernel(FrameArgs a) {
-    const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (t >= a.nchunks) return;
-    uint8_t bad = 0, stop = 0;
-    const uint64_t g = a.g[t];
-    if (g != kNone) {
-        if (a.st[t] == kExit) {
-            const uint64_t x = a.x[t];
-            const uint64_t j = x / a.chunk;
-            if (j >= a.nchunks || a.g[j] != x) bad = 1;
+    } else {
+        const Chase c = chase(a, g, c1, LdsStarts{&s_rec[threadIdx.x], c0});
+        put_chase(a, t, c);
+        if (c.st == kExit) {
+            const uint64_t j = c.x / a.chunk;
+            if (j >= a.nchunks || a.g[j] != c.x) bad = 1;
             for (uint64_t k = t + 1; k < j && !bad; ++k)
                 if (a.g[k] != kNone) bad = 1;
         } else {
             stop = 1;
         }
+        uint64_t* rec = a.starts + t * kStartsCap;
+        for (uint32_t i = 0; i < min(c.cnt, kStartsCap); ++i) rec[i] = c0 + s_rec[i * kChunksWG + threadIdx.x];
     }
     a.fail[t] = bad;
     a.stop[t] = stop;
@@ -552,12 +550,6 @@ hipError_t launch_frame_guess(const FrameArgs& a, hipStream_t s) {
 hipError_t launch_frame_chunks(const FrameArgs& a, hipStream_t s) {
     const uint32_t blocks = uint32_t((a.nchunks + kChunksWG - 1) / kChunksWG);
     ONC_LAUNCH(frame_chunks_kernel, dim3(blocks), dim3(kChunksWG), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_frame_verify(const FrameArgs& a, hipStream_t s) {
-    const uint32_t blocks = uint32_t((a.nchunks + 255) / 256);
-    ONC_LAUNCH(frame_verify_kernel, dim3(blocks), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

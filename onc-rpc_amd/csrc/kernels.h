@@ -126,7 +126,6 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s);
 hipError_t launch_iov_len(const IovArgs& a, hipStream_t s);
 hipError_t launch_iov_emit(const IovArgs& a, hipStream_t s);
 // frame.hip
-hipError_t launch_frame_verify(const FrameArgs& a, hipStream_t s);
 hipError_t launch_frame_walk(const FrameArgs& a, hipStream_t s);
 hipError_t launch_frame_counts(const FrameArgs& a, hipStream_t s);
 hipError_t launch_frame_guess(const FrameArgs& a, hipStream_t s);

@@ -19,11 +19,11 @@ LIB_PATH = os.environ.get("ONC_RPC_AMD_LIB") or os.path.join(os.path.dirname(os.
 
 K_NAMES = ["enc_len_kernel", "scan_tiles_kernel", "enc_emit_kernel", "decode_kernel",
            "len_tiles_kernel", "len_apply_kernel", "iov_len_kernel", "iov_emit_kernel",
-           "frame_chunks_kernel", "frame_write_kernel", "frame_verify_kernel", "frame_walk_kernel",
+           "frame_chunks_kernel", "frame_write_kernel", "frame_coff_kernel", "frame_walk_kernel",
            "frame_counts_kernel", "frame_guess_kernel"]
 (K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY, K_IOV_LEN,
- K_IOV_EMIT, K_FRAME, K_FRAME_WRITE, K_FRAME_VERIFY, K_FRAME_WALK, K_FRAME_COUNTS, K_FRAME_GUESS) = range(14)
-ABI_VERSION = 2
+ K_IOV_EMIT, K_FRAME, K_FRAME_WRITE, K_FRAME_OFFSETS, K_FRAME_WALK, K_FRAME_COUNTS, K_FRAME_GUESS) = range(14)
+ABI_VERSION = 3
 K_COUNT = len(K_NAMES)
 
 # every symbol include/onc_rpc.h declares
