@@ -731,9 +731,12 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
         def step():
             if args.frame:
                 codec.frame_stream(out, total_bytes, dec_off, n, frame_res)
+                codec.decode(out, dec_off, n, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1)
             else:
-                codec.scan_lengths(rec_len, n, 0, dec_off)
-            codec.decode(out, dec_off, n, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1)
+                # offsets from the lengths inside the decode (onc_decode_lengths);
+                # they are also written out (dec_off: the validation below)
+                codec.decode_lengths(out, rec_len, n, 0, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1,
+                                     rec_off=dec_off)
     else:
         def step():
             codec.encode(db, out, rec_off, enc_status)

@@ -409,6 +409,16 @@ int onc_frame_stream(onc_codec* codec, const uint8_t* wire, uint64_t len,
 int onc_scan_lengths(onc_codec* codec, const uint32_t* rec_len, uint64_t n,
                      uint64_t base, uint64_t* rec_off);
 
+/* onc_scan_lengths + onc_decode in one pass: record i is
+ * wire[off_i, off_i + rec_len[i]) with off_0 = base, off_(i+1) = off_i +
+ * rec_len[i] (the caller's length-delimited slices, each decoded as by
+ * TryFrom<&[u8]> / TryFrom<Bytes>, rpc_message.rs:235-314). The offsets are
+ * computed inside the decode (no offsets pass over the batch); rec_off
+ * (optional, n + 1 entries, [dev]) receives them. Same outputs, over-read
+ * rule and errors as onc_decode. */
+int onc_decode_lengths(onc_codec* codec, const uint8_t* wire, const uint32_t* rec_len, uint64_t n,
+                       uint64_t base, int mode, uint64_t* rec_off, const onc_decoded* out);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -5,6 +5,7 @@
 // synchronisation happen inside encode/decode (the caller syncs).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -577,6 +578,45 @@ int onc_decode(onc_codec* c, const uint8_t* wire, const uint64_t* rec_off, uint6
     a.rec_off = rec_off;
     a.out = *out;
     a.variant = c->variant;
+    return run(c, ONC_K_DEC_PARSE, "decode", [&] { return onc::launch_decode(a, mode, c->stream); });
+}
+
+int onc_decode_lengths(onc_codec* c, const uint8_t* wire, const uint32_t* rec_len, uint64_t n, uint64_t base,
+                       int mode, uint64_t* rec_off, const onc_decoded* out) {
+    if (!c || !out || (mode != ONC_DECODE_SLICE && mode != ONC_DECODE_BYTES)) return ONC_RC_EINVAL;
+    if (n == 0) return ONC_RC_OK;
+    if (!rec_len || !out->msgs || !out->unix_params || !out->status || !out->aux0 || !out->aux1)
+        return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    // scratch: 64-record workgroup totals (n / 64 words, within the 3T words
+    // before the block area), 4096-record block totals and their scan
+    const uint64_t wgs = (n + 63) / 64, nblk = (n + onc::kDecLenBlk - 1) / onc::kDecLenBlk;
+    int rc = ensure_scratch(c, std::max<uint64_t>(onc::num_tiles(n), wgs / 3 + 1));
+    if (rc != ONC_RC_OK) return rc;
+    const uint64_t T = c->scratch_tiles;
+    onc::DecArgs a{};
+    a.n = n;
+    a.wire = wire;
+    a.out = *out;
+    a.variant = c->variant;
+    a.rec_len = rec_len;
+    a.tile_sum = c->scratch;
+    a.blk_sum = c->scratch + 3 * T;
+    a.nblk = nblk;
+    a.base = base;
+    a.rec_off_out = rec_off;
+    uint64_t* blk_sum = c->scratch + 3 * T;
+    rc = run(c, ONC_K_LEN_TILES, "dlen_tiles", [&] {
+        return onc::launch_dlen_tiles(rec_len, n, c->scratch, blk_sum, c->stream);
+    });
+    if (rc != ONC_RC_OK) return rc;
+    if (nblk > onc::kDecLenFusedBlocks || c->force_scan) {
+        uint64_t* blk_base = blk_sum + (T / 4 + 1);
+        rc = run(c, ONC_K_SCAN_TILES, "scan_tiles",
+                 [&] { return onc::launch_scan_tiles(blk_sum, blk_base, nblk, 0, nullptr, c->stream); });
+        if (rc != ONC_RC_OK) return rc;
+        a.blk_base = blk_base;
+    }
     return run(c, ONC_K_DEC_PARSE, "decode", [&] { return onc::launch_decode(a, mode, c->stream); });
 }
 

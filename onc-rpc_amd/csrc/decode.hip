@@ -335,7 +335,15 @@ __device__ __forceinline__ int32_t parse_record(const Rd& R, uint64_t L, uint64_
 // (tools/dec_lab.hip: 1 / 2 / 3 / 4 chunks per record, 1M records 300 B
 // apart, cold: 53 / 59 / 65 / 71 us — ~53 us per million lines). Measured
 // c1 decode 59.6 -> 56.0 us, c2 90.1 -> 88.5 us, c3 unchanged.
-template <int MODE, bool kExact = false, bool kNTOut = false>
+// kFromLen (onc_decode_lengths): the record's offset comes from the lengths
+// inside the kernel — the byte totals of the 4096-record blocks before this
+// workgroup's (summed here, or their scan beyond kDecLenFusedBlocks blocks),
+// the totals of the workgroups before it in its block and a wave scan of its
+// own lengths, all loads issued together — instead of an offsets pass over
+// the whole batch (onc_scan_lengths: 8 bytes written and read back per
+// record, one launch more).
+static_assert(kDecTile == 64, "kFromLen: one wave per workgroup, 64 workgroup totals per block");
+template <int MODE, bool kExact = false, bool kNTOut = false, bool kFromLen = false, bool kBlkFused = false>
 __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     __shared__ uint32_t s_win[kWinWords * kDecTile];
     static_assert(kWinWords * kDecTile * 4 >= kDecTile * sizeof(onc_msg), "descriptor staging reuses the window");
@@ -344,7 +352,31 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     const uint64_t i = i0 + t;
     const bool valid = i < a.n;
     uint64_t b = 0, L = 0;
-    if (valid) {
+    if constexpr (kFromLen) {
+        const uint64_t wg = blockIdx.x;
+        const uint64_t blk = wg / (kDecLenBlk / kDecTile);
+        const uint64_t w0 = blk * (kDecLenBlk / kDecTile);
+        const uint32_t len = valid ? a.rec_len[i] : 0u;
+        const uint64_t ts = w0 + t < wg ? a.tile_sum[w0 + t] : 0;
+        uint64_t pre = 0;
+        if constexpr (kBlkFused) {
+#pragma unroll
+            for (int k = 0; k < int(kDecLenFusedBlocks / 64); ++k) {
+                const uint64_t j = uint64_t(t) + 64ull * k;
+                pre += j < blk ? a.blk_sum[j] : 0;
+            }
+        } else {
+            pre = t == 0 ? a.blk_base[blk] : 0;
+        }
+        const uint64_t incl = wave_incl_scan_u64(uint64_t(len));
+        const uint64_t wbase = a.base + lane_u64(wave_incl_scan_u64(pre + ts), 63);
+        b = wbase + incl - len;
+        L = len;
+        if (a.rec_off_out && valid) {
+            a.rec_off_out[i] = b;
+            if (i + 1 == a.n) a.rec_off_out[a.n] = b + L;
+        }
+    } else if (valid) {
         b = a.rec_off[i];
         L = a.rec_off[i + 1] - b;
     }
@@ -460,7 +492,54 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     }
 }
 
+// dlen_tiles: per 4096-record block (256 threads x 16 lengths) the byte
+// total of every 64-record decode workgroup (4 threads) and of the block.
+__global__ __launch_bounds__(256) void dlen_tiles_kernel(const uint32_t* len, uint64_t n, uint64_t* tile_sum,
+                                                         uint64_t* blk_sum) {
+    __shared__ uint64_t s_wave[4];
+    const uint64_t lo = uint64_t(blockIdx.x) * kDecLenBlk + 16ull * threadIdx.x;
+    uint64_t sum = 0;
+    if (lo + 16 <= n && (reinterpret_cast<uintptr_t>(len + lo) & 15) == 0) {
+        const uint4* p = reinterpret_cast<const uint4*>(len + lo);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 w = p[k];
+            sum += uint64_t(w.x) + w.y + w.z + w.w;
+        }
+    } else {
+        for (int k = 0; k < 16; ++k) sum += lo + k < n ? len[lo + k] : 0u;
+    }
+    // groups of 4 threads = one 64-record workgroup
+    const uint64_t incl = wave_incl_scan_u64(sum);
+    const int lane = threadIdx.x & 63;
+    const uint64_t prev4_all = __shfl(incl, (lane + 60) & 63, 64);   // lane - 4 (wrapping)
+    const uint64_t prev4 = lane >= 4 ? prev4_all : 0;
+    const uint64_t wgi = (uint64_t(blockIdx.x) * kDecLenBlk + 64ull * (threadIdx.x >> 2)) / kDecTile;
+    if ((lane & 3) == 3 && wgi * kDecTile < n) tile_sum[wgi] = incl - prev4;
+    uint64_t total;
+    block_excl_scan_u64<256>(sum, s_wave, &total);
+    if (threadIdx.x == 0) blk_sum[blockIdx.x] = total;
+}
+
+hipError_t launch_dlen_tiles(const uint32_t* rec_len, uint64_t n, uint64_t* tile_sum, uint64_t* blk_sum, hipStream_t s) {
+    ONC_LAUNCH(dlen_tiles_kernel, dim3(uint32_t((n + kDecLenBlk - 1) / kDecLenBlk)), dim3(256), 0, s, rec_len, n, tile_sum,
+               blk_sum);
+    return hipGetLastError();
+}
+
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s) {
+    if (a.rec_len) {
+        const uint64_t wgs = (a.n + kDecTile - 1) / kDecTile;
+        const bool fused = a.blk_base == nullptr;
+        if (mode == ONC_DECODE_BYTES) {
+            if (fused) ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true, true, true>), dim3(uint32_t(wgs)), dim3(kDecTile), 0, s, a);
+            else ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true, true, false>), dim3(uint32_t(wgs)), dim3(kDecTile), 0, s, a);
+        } else {
+            if (fused) ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true, true, true>), dim3(uint32_t(wgs)), dim3(kDecTile), 0, s, a);
+            else ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true, true, false>), dim3(uint32_t(wgs)), dim3(kDecTile), 0, s, a);
+        }
+        return hipGetLastError();
+    }
     const uint64_t tiles = (a.n + kDecTile - 1) / kDecTile;
     if (mode == ONC_DECODE_BYTES)
         ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true>), dim3(uint32_t(tiles)), dim3(kDecTile), 0, s, a);

@@ -117,7 +117,17 @@ struct DecArgs {
     const uint64_t* rec_off;
     onc_decoded out;
     uint32_t variant;       // ONC_RPC_VARIANT bits (A/B experiments)
+    // onc_decode_lengths: offsets from the lengths inside the decode
+    const uint32_t* rec_len;
+    const uint64_t* tile_sum;   // per decode workgroup (kDecTile records): byte total
+    const uint64_t* blk_sum;    // per 4096 records: byte total (summed in the kernel) ...
+    const uint64_t* blk_base;   // ... or their exclusive scan (beyond kDecLenFusedBlocks blocks)
+    uint64_t nblk;
+    uint64_t base;              // offset of record 0
+    uint64_t* rec_off_out;      // optional: the offsets (n + 1)
 };
+constexpr uint64_t kDecLenBlk = 4096;          // records per length block
+constexpr uint64_t kDecLenFusedBlocks = 512;   // up to 2M records: block totals summed in the decode
 
 // encode.hip
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s);
@@ -147,6 +157,7 @@ hipError_t launch_lenoff(const uint32_t* len, uint64_t n, const uint64_t* blk_su
                          hipStream_t s);
 // decode.hip
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s);
+hipError_t launch_dlen_tiles(const uint32_t* rec_len, uint64_t n, uint64_t* tile_sum, uint64_t* blk_sum, hipStream_t s);
 
 __host__ __device__ inline uint64_t num_tiles(uint64_t n) { return (n + 255) / 256; }
 __host__ __device__ inline uint64_t num_len_blocks(uint64_t n) { return (n + kLenRecs - 1) / kLenRecs; }

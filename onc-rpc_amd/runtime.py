@@ -33,6 +33,7 @@ EXPORTED = [
     "onc_codec_enable_timing", "onc_codec_kernel_stats", "onc_codec_reset_stats",
     "onc_kernel_name", "onc_encode_lengths", "onc_encode", "onc_decode", "onc_scan_lengths",
     "onc_expected_message_len", "onc_encode_iov", "onc_frame_stream", "onc_encode_plan", "onc_encode_emit",
+    "onc_decode_lengths",
 ]
 
 
@@ -80,6 +81,7 @@ def load_library(path=LIB_PATH):
     lib.onc_encode_plan.argtypes = [vp, C.POINTER(OncBatch), vp, vp]
     lib.onc_encode_emit.argtypes = [vp, C.POINTER(OncBatch), vp, u64, vp, vp]
     lib.onc_decode.argtypes = [vp, vp, vp, u64, i32, C.POINTER(OncDecoded)]
+    lib.onc_decode_lengths.argtypes = [vp, vp, vp, u64, u64, i32, vp, C.POINTER(OncDecoded)]
     lib.onc_scan_lengths.argtypes = [vp, vp, u64, u64, vp]
     lib.onc_frame_stream.argtypes = [vp, vp, u64, vp, u64, vp]
     lib.onc_encode_iov.argtypes = [vp, C.POINTER(OncBatch), vp, u64, vp, vp, vp]
@@ -245,6 +247,15 @@ class Codec:
                        aux1.data_ptr())
         self._check(self.lib.onc_decode(self.h, _ptr(wire), _ptr(rec_off), n, mode, C.byref(d)),
                     "onc_decode")
+
+    def decode_lengths(self, wire, rec_len, n, base, mode, msgs, unix, status, aux0, aux1, rec_off=None):
+        """onc_decode_lengths: offsets from rec_len inside the decode (rec_off
+        optional: receives them, n + 1 entries)."""
+        d = OncDecoded(msgs.data_ptr(), unix.data_ptr(), status.data_ptr(), aux0.data_ptr(),
+                       aux1.data_ptr())
+        self._check(self.lib.onc_decode_lengths(self.h, _ptr(wire), _ptr(rec_len), n, base, mode,
+                                                _ptr(rec_off) if rec_off is not None else None, C.byref(d)),
+                    "onc_decode_lengths")
 
     def scan_lengths(self, rec_len, n, base, rec_off):
         self._check(self.lib.onc_scan_lengths(self.h, _ptr(rec_len), n, base, _ptr(rec_off)),
