@@ -90,21 +90,52 @@ struct Rules {
 // to memory as a partial line (c3 decode 450 -> 1040-1300 us); for sparse
 // slots (configs[2]: a quarter of the records) the two policies measured
 // within the run-to-run spread.
-__device__ __forceinline__ void put_unix(onc_unix_params* u, uint32_t stamp, uint32_t uid, uint32_t gid,
-                                         uint32_t ng, uint64_t name_off, uint32_t nl, const uint32_t* gids,
-                                         uint32_t pad) {
-    uint4* d = reinterpret_cast<uint4*>(u);
-    if (pad == 2) {
-        d[-2] = make_uint4(0, 0, 0, 0);
-        d[-1] = make_uint4(0, 0, 0, 0);
-    }
-    d[0] = make_uint4(stamp, uid, gid, ng);
-    d[1] = make_uint4(uint32_t(name_off), uint32_t(name_off >> 32), nl, 0u);
+// AUTH_UNIX parameters of a record's credential (slot 2i, k = 0) and
+// verifier (slot 2i + 1, k = 1), held in registers until the record is
+// parsed, then written out (see the end of decode_kernel): 24 words per
+// slot in onc_unix_params order.
+struct UnixSlots {
+    uint32_t w[2][24];
+    uint32_t mask;      // bit k: slot k holds parameters
+};
+__device__ __forceinline__ void put_unix(UnixSlots& us, int k, uint32_t stamp, uint32_t uid, uint32_t gid,
+                                         uint32_t ng, uint64_t name_off, uint32_t nl, const uint32_t* gids) {
+    us.w[k][0] = stamp;
+    us.w[k][1] = uid;
+    us.w[k][2] = gid;
+    us.w[k][3] = ng;
+    us.w[k][4] = uint32_t(name_off);
+    us.w[k][5] = uint32_t(name_off >> 32);
+    us.w[k][6] = nl;
+    us.w[k][7] = 0u;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) d[2 + k] = make_uint4(gids[4 * k], gids[4 * k + 1], gids[4 * k + 2], gids[4 * k + 3]);
-    if (pad == 1) {
-        d[6] = make_uint4(0, 0, 0, 0);
-        d[7] = make_uint4(0, 0, 0, 0);
+    for (int g = 0; g < 16; ++g) us.w[k][8 + g] = gids[g];
+    us.mask |= 1u << k;
+}
+
+// One lane's slots straight to global memory (waves with few AUTH_UNIX
+// records), padded to whole 64-byte sectors: the credential slot with the
+// verifier slot's first 32 bytes zeroed (when that slot has no parameters),
+// the verifier slot with the credential slot's last 32 bytes zeroed (when
+// that one has none) — partial 64-byte sectors cost a read-modify-write
+// (c3 decode 537 -> 454 us with the padding).
+__device__ __forceinline__ void put_unix_direct(onc_unix_params* pair, const UnixSlots& us) {
+    uint4* d = reinterpret_cast<uint4*>(pair);          // 12 x 16 bytes: [cred 0..5][verf 6..11]
+    if (us.mask & 1u) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) d[q] = make_uint4(us.w[0][4 * q], us.w[0][4 * q + 1], us.w[0][4 * q + 2], us.w[0][4 * q + 3]);
+        if (!(us.mask & 2u)) {
+            d[6] = make_uint4(0, 0, 0, 0);
+            d[7] = make_uint4(0, 0, 0, 0);
+        }
+    }
+    if (us.mask & 2u) {
+        if (!(us.mask & 1u)) {
+            d[4] = make_uint4(0, 0, 0, 0);
+            d[5] = make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 6; ++q) d[6 + q] = make_uint4(us.w[1][4 * q], us.w[1][4 * q + 1], us.w[1][4 * q + 2], us.w[1][4 * q + 3]);
     }
 }
 
@@ -112,7 +143,7 @@ __device__ __forceinline__ void put_unix(onc_unix_params* u, uint32_t stamp, uin
 // AuthUnixParams::from_cursor (unix_params.rs:90-129) and
 // Opaque::from_wire (opaque.rs:72-98; bound = the whole message, `end`).
 __device__ __forceinline__ int32_t auth_slice(const Rd& R, uint32_t& pos, uint32_t end, uint64_t rec_off,
-                                              uint64_t slot, onc_auth& a, onc_unix_params* uo, uint32_t pad) {
+                                              uint64_t slot, onc_auth& a, UnixSlots& us) {
     constexpr int32_t kShort = Rules<ONC_DECODE_SLICE>::kShort;
     uint32_t fl;
     ONC_RD(fl);
@@ -141,7 +172,7 @@ __device__ __forceinline__ int32_t auth_slice(const Rd& R, uint32_t& pos, uint32
             gids[g] = v;
         }
         if (pos - start != n) return ONC_ERR_INVALID_AUTH_DATA;          // unix_params.rs:117-119
-        put_unix(uo + slot, stamp, uid, gid, ng, rec_off + name_pos, nl, gids, pad);
+        put_unix(us, int(slot & 1), stamp, uid, gid, ng, rec_off + name_pos, nl, gids);
         a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
         a.ref = slot;
         return ONC_OK;
@@ -161,7 +192,7 @@ __device__ __forceinline__ int32_t auth_slice(const Rd& R, uint32_t& pos, uint32
 // first cut with try_array(200) (bytes_ext.rs:25-42); AUTH_UNIX is parsed
 // inside that slice (unix_params.rs:252-276) and must fill it exactly.
 __device__ __forceinline__ int32_t auth_bytes(const Rd& R, uint32_t& pos, uint32_t end, uint64_t rec_off,
-                                              uint64_t slot, onc_auth& a, onc_unix_params* uo, uint32_t pad) {
+                                              uint64_t slot, onc_auth& a, UnixSlots& us) {
     constexpr int32_t kShort = Rules<ONC_DECODE_BYTES>::kShort;
     uint32_t fl, n;
     ONC_RD(fl);
@@ -200,7 +231,7 @@ __device__ __forceinline__ int32_t auth_bytes(const Rd& R, uint32_t& pos, uint32
 #undef ONC_RDQ
         // params.serialised_len() != auth_data.len() -> InvalidAuthData (flavor.rs:204-208)
         if (20u + nl + pad4(nl) + 4u * ng != n) return ONC_ERR_INVALID_AUTH_DATA;
-        put_unix(uo + slot, stamp, uid, gid, ng, rec_off + name_pos, nl, gids, pad);
+        put_unix(us, int(slot & 1), stamp, uid, gid, ng, rec_off + name_pos, nl, gids);
         a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
         a.ref = slot;
         return ONC_OK;
@@ -213,16 +244,16 @@ __device__ __forceinline__ int32_t auth_bytes(const Rd& R, uint32_t& pos, uint32
 
 template <int MODE>
 __device__ __forceinline__ int32_t auth_any(const Rd& R, uint32_t& pos, uint32_t end, uint64_t rec_off,
-                                            uint64_t slot, onc_auth& a, onc_unix_params* uo, uint32_t pad) {
-    if (MODE == ONC_DECODE_BYTES) return auth_bytes(R, pos, end, rec_off, slot, a, uo, pad);
-    return auth_slice(R, pos, end, rec_off, slot, a, uo, pad);
+                                            uint64_t slot, onc_auth& a, UnixSlots& us) {
+    if (MODE == ONC_DECODE_BYTES) return auth_bytes(R, pos, end, rec_off, slot, a, us);
+    return auth_slice(R, pos, end, rec_off, slot, a, us);
 }
 
 // RpcMessage::try_from (rpc_message.rs:243-271 / :277-313), flattened.
 template <int MODE>
 __device__ __forceinline__ int32_t parse_record(const Rd& R, uint64_t L, uint64_t rec_off, uint64_t i,
                                                 onc_msg& m, uint32_t& aux0, uint32_t& aux1,
-                                                onc_unix_params* uo) {
+                                                UnixSlots& us) {
     constexpr int32_t kShort = Rules<MODE>::kShort;
     // expected_message_len (rpc_message.rs:343-367) + exact-length check
     if (L < 4) return ONC_ERR_INCOMPLETE_HEADER;
@@ -250,10 +281,9 @@ __device__ __forceinline__ int32_t parse_record(const Rd& R, uint64_t L, uint64_
         ONC_RD(m.u.call.program);
         ONC_RD(m.u.call.program_version);
         ONC_RD(m.u.call.procedure);
-        int32_t st = auth_any<MODE>(R, pos, end, rec_off, 2 * i, m.cred, uo, 1u);
+        int32_t st = auth_any<MODE>(R, pos, end, rec_off, 2 * i, m.cred, us);
         if (st != ONC_OK) return st;
-        const uint32_t vpad = (m.cred.kind_len >> 24) == ONC_KIND_UNIX ? 0u : 2u;
-        st = auth_any<MODE>(R, pos, end, rec_off, 2 * i + 1, m.verf, uo, vpad);
+        st = auth_any<MODE>(R, pos, end, rec_off, 2 * i + 1, m.verf, us);
         if (st != ONC_OK) return st;
         m.payload_off = rec_off + pos;                     // call_body.rs:53-59 (zero copy)
         m.payload_len = end - pos;
@@ -267,7 +297,7 @@ __device__ __forceinline__ int32_t parse_record(const Rd& R, uint64_t L, uint64_
     ONC_RD(v);
     if (v == ONC_REPLY_ACCEPTED) {
         m.reply_stat = ONC_REPLY_ACCEPTED;
-        const int32_t st = auth_any<MODE>(R, pos, end, rec_off, 2 * i + 1, m.verf, uo, 2u);
+        const int32_t st = auth_any<MODE>(R, pos, end, rec_off, 2 * i + 1, m.verf, us);
         if (st != ONC_OK) return st;
         ONC_RD(v);
         m.stat = uint8_t(v);
@@ -456,8 +486,10 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);
     uint32_t aux0 = 0, aux1 = 0;
     int32_t st = ONC_OK;
+    UnixSlots us;
+    us.mask = 0;
     if (valid) {
-        st = parse_record<MODE>(R, L, b, i, m, aux0, aux1, a.out.unix_params);
+        st = parse_record<MODE>(R, L, b, i, m, aux0, aux1, us);
         if (st != ONC_OK) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);
@@ -473,6 +505,49 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
         }
     }
     __syncthreads();                                  // every lane is done with its window
+    // AUTH_UNIX slots. When at least half the workgroup's records carry
+    // parameters, the slot pairs of 32 records at a time (6 KiB, contiguous
+    // in the output) are staged in the window and written as whole lines
+    // with nontemporal stores: per-lane 16-byte stores 192 bytes apart touch
+    // 64 lines per instruction (configs[3] decode 456 us with them, 275 us
+    // with no slot stores at all). Otherwise each lane writes its own.
+    const uint64_t um = __ballot(us.mask != 0);
+    if (um) {
+        static_assert(kDecTile == 64, "slot staging: one wave, two halves of 32 records");
+        if (__popcll(um) >= 32) {
+            uint4* stg = reinterpret_cast<uint4*>(s_win);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (h) __syncthreads();                   // the first half's stores have read the window
+                if ((t >> 5) == h) {
+                    uint4* d = stg + 12 * (t & 31);
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const bool on = (us.mask >> k) & 1u;
+#pragma unroll
+                        for (int q = 0; q < 6; ++q)
+                            d[6 * k + q] = on ? make_uint4(us.w[k][4 * q], us.w[k][4 * q + 1], us.w[k][4 * q + 2],
+                                                           us.w[k][4 * q + 3])
+                                              : make_uint4(0, 0, 0, 0);
+                    }
+                }
+                __syncthreads();
+                const uint64_t r0 = i0 + 32ull * h;
+                uint4* dst = reinterpret_cast<uint4*>(a.out.unix_params + 2 * r0);
+#pragma unroll
+                for (int c = 0; c < 6; ++c) {
+                    const uint32_t q = uint32_t(t + 64 * c);      // 16-byte chunk of the 6 KiB; record q / 12
+                    if (r0 + q / 12 < a.n) {
+                        const uint4 v = stg[q];
+                        __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst + q));
+                    }
+                }
+            }
+            __syncthreads();                              // the window is reused below
+        } else if (us.mask) {
+            put_unix_direct(a.out.unix_params + 2 * i, us);
+        }
+    }
     uint4* stage = reinterpret_cast<uint4*>(s_win);
 #pragma unroll
     for (int k = 0; k < 4; ++k) stage[4 * t + k] = mz[k];
