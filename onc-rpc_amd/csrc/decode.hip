@@ -507,10 +507,12 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     __syncthreads();                                  // every lane is done with its window
     // AUTH_UNIX slots. When at least half the workgroup's records carry
     // parameters, the slot pairs of 32 records at a time (6 KiB, contiguous
-    // in the output) are staged in the window and written as whole lines
-    // with nontemporal stores: per-lane 16-byte stores 192 bytes apart touch
-    // 64 lines per instruction (configs[3] decode 456 us with them, 275 us
-    // with no slot stores at all). Otherwise each lane writes its own.
+    // in the output) are staged in the window and written with coalesced
+    // nontemporal stores, skipping the 64-byte sectors of slots without
+    // parameters: per-lane 16-byte stores 192 bytes apart touch 64 lines per
+    // instruction (configs[3] decode 473 us with them, 411 us staged with
+    // every sector, 275 us with no slot stores at all). Otherwise each lane
+    // writes its own.
     const uint64_t um = __ballot(us.mask != 0);
     if (um) {
         static_assert(kDecTile == 64, "slot staging: one wave, two halves of 32 records");
@@ -537,7 +539,12 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
 #pragma unroll
                 for (int c = 0; c < 6; ++c) {
                     const uint32_t q = uint32_t(t + 64 * c);      // 16-byte chunk of the 6 KiB; record q / 12
-                    if (r0 + q / 12 < a.n) {
+                    const uint32_t rr = q / 12, p = q - 12 * rr;  // chunk p of the record's 192-byte pair
+                    const uint32_t mk = uint32_t(__shfl(int(us.mask), int(32 * h + rr), 64));
+                    // whole 64-byte sectors only where a slot has parameters:
+                    // [0, 64) credential, [128, 192) verifier, [64, 128) either
+                    const bool need = p < 4 ? (mk & 1u) : (p >= 8 ? (mk & 2u) : mk != 0);
+                    if (r0 + rr < a.n && need) {
                         const uint4 v = stg[q];
                         __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst + q));
                     }
