@@ -36,7 +36,10 @@ constexpr uint32_t kWinWords = 4 * kWinChunks;
 #ifndef ONC_DEC_TILE
 #define ONC_DEC_TILE 64     // c1 decode 54.7 -> 50.2 us, c2 81 -> 78.6, c3 447 -> 468 vs 256 (profiles/lab_r02_dec_tile.log)
 #endif
-constexpr int kDecTile = ONC_DEC_TILE;        // records (lanes) per decode workgroup
+constexpr int kDecTile = ONC_DEC_TILE;
+#ifndef ONC_DEC_STAGE_MIN
+#define ONC_DEC_STAGE_MIN 32   // AUTH_UNIX records in a workgroup from which its slots are staged
+#endif        // records (lanes) per decode workgroup
 
 struct Rd {
     uintptr_t base;          // absolute address of record byte 0
@@ -516,7 +519,7 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     const uint64_t um = __ballot(us.mask != 0);
     if (um) {
         static_assert(kDecTile == 64, "slot staging: one wave, two halves of 32 records");
-        if (__popcll(um) >= 32) {
+        if (__popcll(um) >= ONC_DEC_STAGE_MIN) {
             uint4* stg = reinterpret_cast<uint4*>(s_win);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
