@@ -498,6 +498,8 @@ class Timing:
         # a timed launch still costs the step ~6 us of dispatch serialisation
         # (the profiling completion signal), which is not the kernel's work.
         self.stride = max(1, steps // 5)
+        if os.environ.get("ONC_BENCH_TIMED_STRIDE"):      # lab: how the timed-launch stride perturbs the step
+            self.stride = max(1, int(os.environ["ONC_BENCH_TIMED_STRIDE"]))
         t_wall0 = time.perf_counter()
         ev0.record()
         for i in range(steps):
