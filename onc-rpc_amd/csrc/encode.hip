@@ -598,8 +598,9 @@ struct WsLane {
 // per lane), then the tile totals before the tile inside its workgroup.
 constexpr uint64_t kTilesPerBlk = kLenRecs / kEmitRecs;
 // A tile's prologue loads (its workgroup's tile totals, the workgroup totals
-// since the producer's previous tile, its descriptors), issued one tile
-// ahead: the producer's next tile is in flight across the barrier.
+// since the producer's previous tile, its descriptors), issued together.
+// (Issuing them a phase ahead, in flight across the barrier, measured no
+// faster.)
 struct WsLoads {
     MsgRegs mr;
     uint64_t tv, bw;
@@ -802,9 +803,6 @@ __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile
     }
 }
 
-#ifndef ONC_WS_PREFETCH
-#define ONC_WS_PREFETCH 0     // the producer's next tile issued a phase ahead: measured no faster
-#endif
 #ifndef ONC_WS_U
 #define ONC_WS_U 2            // consumer chunks per lane per step (c1: 2 -> enc_emit 121 -> 116 us vs 1)
 #endif
@@ -826,30 +824,21 @@ __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
     S.run_base = 0;
     uint64_t next = blockIdx.x;
     bool have = false;
-    WsLoads pf;
-    bool need_pf = false;
-    if (ONC_WS_PREFETCH && wv == 0 && next < ntiles) pf = ws_issue(a, 0, next);
-
     // producer: one span into slot W, or "done"
     const auto produce = [&](WsSlot& W) {
         if (!have && next < ntiles) {
-            if (!ONC_WS_PREFETCH) pf = ws_issue(a, S.run_blk, next);
+            WsLoads pf = ws_issue(a, S.run_blk, next);
             asm volatile("" : "+v"(pf.mr.q[0]), "+v"(pf.mr.q[1]), "+v"(pf.mr.q[2]), "+v"(pf.mr.q[3]), "+v"(pf.tv),
                          "+v"(pf.bw));
             ws_begin_tile(a, S, s_ln, next, pf);
             next += gridDim.x;
             have = true;
-            need_pf = next < ntiles;
         }
         if (!have) {
             if ((threadIdx.x & 63) == 0) W.h.state = 2u;
             return;
         }
         ws_stage_span(a, S, s_ln, W);
-        // issued after the span's own loads: one in-order vmcnt, so waiting
-        // for those must not wait for these
-        if (ONC_WS_PREFETCH && need_pf) pf = ws_issue(a, S.run_blk, next);
-        need_pf = false;
         if (S.lo_rec >= S.nrec) have = false;
     };
 #ifdef ONC_EMIT_PROF
