@@ -560,11 +560,13 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
 // wave 0 (the producer) does everything enc_emit_tile does before the
 // stream — placement, plan, scans, the span's LDS image and maps — for the
 // next span into one slot while waves 1-3 (the consumers) stream the
-// previous span out of the other slot, interleaved by 1 KiB steps (consumer
-// c takes steps c, c + 3, ...). One workgroup barrier per span. The wave-
-// per-tile kernel keeps ~26 % of every tile's life in staging with no
-// memory traffic, and its tiles start in lock-step rounds, so those phases
-// coincide chip-wide; here the streams never stop for staging.
+// previous span out of the other slot, interleaved by steps of 64 * kU
+// chunks (consumer c takes steps c, c + 3, ...; kU = 2, or 1 for payloads
+// averaging >= 512 bytes). One workgroup barrier per span. The wave-per-
+// tile kernel keeps ~26 % of every tile's life in staging with no memory
+// traffic, and its tiles start in lock-step rounds, so those phases
+// coincide chip-wide; here the streams never stop for staging. Chosen per
+// batch by codec.hip (enc_args); DESIGN.md §4 has the measurements.
 struct SpanHdr {
     uint64_t B0, S0, E;
     int32_t NCe;
