@@ -374,9 +374,10 @@ def pcie_pipelined(args, torch, R, wl, hb, db, out, total_bytes, lens_np, rec_le
                 cp_out = [(h_wire[base[k]:base[k] + wb], wire[base[k]:base[k] + wb]),
                           (h_offk[lo + k:hi + k + 1], ok_), (h_st[lo:hi], st[lo:hi]),
                           (h_dec[0][64 * lo:64 * hi], dec.msgs[64 * lo:64 * hi]),
-                          (h_dec[1][192 * lo:192 * hi], dec.unix[192 * lo:192 * hi]),
                           (h_dec[2][lo:hi], dec.status[lo:hi]), (h_dec[3][lo:hi], dec.aux0[lo:hi]),
                           (h_dec[4][lo:hi], dec.aux1[lo:hi])]
+                if u_hi > u_lo:     # the chunk has AUTH_UNIX auths: their decoded slots come back
+                    cp_out.append((h_dec[1][192 * lo:192 * hi], dec.unix[192 * lo:192 * hi]))
             copy_out(cp_out)
             bytes_h2d += sum(h.numel() * h.element_size() for _, h in cp_in)
             bytes_d2h += sum(h.numel() * h.element_size() for h, _ in cp_out)
@@ -415,7 +416,8 @@ def pcie_pipelined(args, torch, R, wl, hb, db, out, total_bytes, lens_np, rec_le
             "pcie_GBs_per_gpu": (bytes_h2d + bytes_d2h) / (pms / 1e3) / 1e9, "chunks": K,
             "validated": ok and float(pt[1]) == 0.0,
             "note": "host wall clock; %d record chunks through copy-in / kernel / copy-out streams: H2D, "
-                    "kernels and D2H of neighbouring chunks overlap" % K}
+                    "kernels and D2H of neighbouring chunks overlap; decoded AUTH_UNIX slots copied back for "
+                    "chunks with AUTH_UNIX auths" % K}
 
 
 # ---------------------------------------------------------------------------
@@ -779,7 +781,12 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
             d_out = [dec_off, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1]
         else:
             d_in = [db.msgs, db.unix, db.auth_arena, db.payload_arena]
-            d_out = [out, rec_off, enc_status, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1]
+            # decoded AUTH_UNIX slots come back only if the batch has AUTH_UNIX
+            # auths: no other record references a slot (onc_decoded.unix_params)
+            kinds = np.concatenate([hb.msgs["cred_kind_len"] >> 24, hb.msgs["verf_kind_len"] >> 24])
+            has_unix = bool((kinds == L.KIND_UNIX).any())
+            d_out = [out, rec_off, enc_status, dec.msgs] + ([dec.unix] if has_unix else []) + \
+                    [dec.status, dec.aux0, dec.aux1]
         h_in = [x.cpu().pin_memory() for x in d_in]
         h_out = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in d_out]
         bytes_h2d = sum(x.numel() * x.element_size() for x in h_in)
@@ -809,7 +816,8 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
         pcie = {"value": n_total / (pms / 1e3) / 1e6, "unit": "Mmsgs/s", "ms_per_step": pms,
                 "h2d_bytes_per_gpu": bytes_h2d, "d2h_bytes_per_gpu": bytes_d2h,
                 "pcie_GBs_per_gpu": (bytes_h2d + bytes_d2h) / (pms / 1e3) / 1e9,
-                "note": "pinned host buffers; H2D, kernels and D2H serialized on one stream"}
+                "note": "pinned host buffers; H2D, kernels and D2H serialized on one stream; decoded AUTH_UNIX "
+                        "slots copied back when the batch has AUTH_UNIX auths"}
         pcie["pipelined"] = pcie_pipelined(args, torch, R, wl, hb, db, out, total_bytes, lens_np, rec_len,
                                            dec_off, dec, mode, h_in, local_rank, dist, n_total)
 
