@@ -72,7 +72,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = every core available)")
     ap.add_argument("--pcie-reps", type=int, default=3)
-    ap.add_argument("--pcie-chunks", type=int, default=4,
+    ap.add_argument("--pcie-chunks", type=int, default=8,
                     help="record chunks of the pipelined PCIe-inclusive leg (two streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
