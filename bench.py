@@ -66,6 +66,9 @@ def parse(argv=None):
     ap.add_argument("--mode", choices=["slice", "bytes"], default="slice")
     ap.add_argument("--frame", action="store_true",
                     help="c2: frame the raw stream on the device (onc_frame_stream) instead of scanning rec_len")
+    ap.add_argument("--iov", action="store_true",
+                    help="c0/c1/c3: the step is the vectored encode (onc_encode_iov: packed headers + one iovec "
+                         "per record, payloads referenced in place) instead of encode + decode")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend of the ranks (control plane only)")
     ap.add_argument("--check-launch", action="store_true",
                     help="start the ranks, check the world size and print it; no GPU work (launcher test)")
@@ -432,6 +435,8 @@ def cdev(dev):
     return dev if BACKEND[0] == "nccl" else "cpu"
 
 
+ALG_CTX = {"unix_refs": 0}     # AUTH_UNIX auths of the batch (iov_emit's parameter-block reads)
+
 ALG_PER_LAUNCH = {
     # algorithmic bytes per launch: encode reads ~W and writes
     # W; zero-copy decode reads H + 4 (the length) and writes ~H.
@@ -441,8 +446,12 @@ ALG_PER_LAUNCH = {
     "decode_kernel": lambda n, W, H: 2 * H + 4 * n,
     "len_tiles_kernel": lambda n, W, H: 4 * n,
     "len_apply_kernel": lambda n, W, H: 12 * n,
-    "iov_len_kernel": lambda n, W, H: 0,
-    "iov_emit_kernel": lambda n, W, H: 0,
+    # vectored encode (H here = the packed header bytes): descriptors read by
+    # both kernels, status written by iov_len; iov_emit reads the wire-carried
+    # data once (descriptor + the 96-byte parameter block of every AUTH_UNIX
+    # auth) and writes the headers + 32-byte iovecs
+    "iov_len_kernel": lambda n, W, H: n * (64 + 4),
+    "iov_emit_kernel": lambda n, W, H: n * (64 + 32) + H + 96 * ALG_CTX["unix_refs"],
     "frame_chunks_kernel": lambda n, W, H: 0,
     "frame_write_kernel": lambda n, W, H: 8 * n,
     "frame_coff_kernel": lambda n, W, H: 0,
@@ -683,6 +692,37 @@ def run_c4(args, torch, R, S, SH, L, dist, rank, world, local_rank, total, mode,
     return res
 
 
+def validate_iov(torch, n, iov, hdr_out, iov_tot, iov_status, wire, rec_off, hdr_len_ref, plen, hb, total_bytes,
+                 hdr_total, dev):
+    """The vectored encode against the contiguous encode of the same batch:
+    every iovec {hdr_off, payload_off, wire_off, hdr_len, payload_len} and
+    every byte of the packed headers (gathered from the wire on the device)."""
+    import numpy as np
+    if int((iov_status[:n] != 0).sum()) or int(iov_tot[0]) != hdr_total or int(iov_tot[1]) != total_bytes:
+        return False
+    e = iov[: 32 * n].view(torch.int64).view(n, 4)
+    hoff, poff, woff = e[:, 0], e[:, 1], e[:, 2]
+    hl = e[:, 3] & 0xFFFFFFFF
+    pl = (e[:, 3] >> 32) & 0xFFFFFFFF
+    if not torch.equal(woff, rec_off[:n]) or not torch.equal(hl, hdr_len_ref) or not torch.equal(pl, plen):
+        return False
+    want_poff = torch.from_numpy(hb.msgs["payload_off"].astype(np.int64)).to(dev)
+    if not torch.equal(poff, want_poff):
+        return False
+    if not torch.equal(hoff, torch.cumsum(hl, 0) - hl):
+        return False
+    ok = True
+    step = 1 << 26                              # header bytes per gather slice
+    for p0 in range(0, hdr_total, step):
+        p = torch.arange(p0, min(hdr_total, p0 + step), dtype=torch.int64, device=dev)
+        r = torch.searchsorted(hoff, p, right=True) - 1
+        src = woff[r] + (p - hoff[r])
+        if not torch.equal(hdr_out[p], wire[src]):
+            ok = False
+            break
+    return ok
+
+
 # ---------------------------------------------------------------------------
 # c0..c3
 # ---------------------------------------------------------------------------
@@ -741,6 +781,25 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
                 # they are also written out (dec_off: the validation below)
                 codec.decode_lengths(out, rec_len, n, 0, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1,
                                      rec_off=dec_off)
+    elif args.iov:
+        # vectored encode; the contiguous encode of the same batch (untimed) is
+        # the reference its headers and iovecs are checked against below
+        codec.encode(db, out, rec_off, enc_status)
+        plen = torch.from_numpy(hb.msgs["payload_len"].astype(np.int64)).to(dev)
+        hdr_len_ref = rec_len[:n].to(torch.int64) & 0xFFFFFFFF
+        hdr_len_ref = hdr_len_ref - torch.where(hdr_len_ref > 0, plen, torch.zeros_like(plen))
+        iov_hdr_total = int(hdr_len_ref.sum())
+        hdr_out = torch.zeros(iov_hdr_total + 16, dtype=torch.uint8, device=dev)
+        iov = torch.zeros(max(n, 1) * 32, dtype=torch.uint8, device=dev)
+        iov_tot = torch.zeros(2, dtype=torch.int64, device=dev)
+        iov_status = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        sum_H = iov_hdr_total
+        ALG_CTX["unix_refs"] = int(((hb.msgs["cred_kind_len"] >> 24) == L.KIND_UNIX).sum() +
+                                   ((hb.msgs["verf_kind_len"] >> 24) == L.KIND_UNIX).sum())
+        desc = desc.replace("encode -> decode", "vectored encode (packed headers + iovecs, payloads in place)")
+
+        def step():
+            codec.encode_iov(db, hdr_out, iov, iov_status, iov_tot, iov_hdr_total)
     else:
         def step():
             codec.encode(db, out, rec_off, enc_status)
@@ -760,22 +819,28 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
     ok = True
     if wl != "c2" and int((enc_status[:n] != 0).sum()):
         ok = False
-    if int((dec.status[:n] != 0).sum()):
-        ok = False
-    if int(dec_off[n]) != total_bytes:
-        ok = False
-    xid = dec.msgs.view(-1, 64)[:n, 0:4].contiguous().view(torch.int32).view(-1)
-    want_xid = torch.from_numpy(hb.msgs["xid"].view(np.int32).copy()).to(dev)
-    if not torch.equal(xid, want_xid):
-        ok = False
+    if args.iov:
+        # every iovec and every packed header byte against the contiguous wire
+        ok = ok and validate_iov(torch, n, iov, hdr_out, iov_tot, iov_status, out, rec_off, hdr_len_ref, plen,
+                                 hb, total_bytes, iov_hdr_total, dev)
+    else:
+        if int((dec.status[:n] != 0).sum()):
+            ok = False
+        if int(dec_off[n]) != total_bytes:
+            ok = False
+        xid = dec.msgs.view(-1, 64)[:n, 0:4].contiguous().view(torch.int32).view(-1)
+        want_xid = torch.from_numpy(hb.msgs["xid"].view(np.int32).copy()).to(dev)
+        if not torch.equal(xid, want_xid):
+            ok = False
     # global placement of this rank's shard in the job's send buffer
-    totals = SH.allgather_totals(int(dec_off[n])) if dist is not None else [int(dec_off[n])]
+    shard_bytes = total_bytes if args.iov else int(dec_off[n])
+    totals = SH.allgather_totals(shard_bytes) if dist is not None else [shard_bytes]
     bases, grand = SH.exclusive_bases(totals)
     ok = agree(torch, dist, dev, ok)
 
     # PCIe-inclusive rate: pinned host inputs -> H2D -> step -> D2H outputs.
     pcie = None
-    if not args.no_pcie:
+    if not args.no_pcie and not args.iov:
         if wl == "c2":
             d_in = [out, rec_len]
             d_out = [dec_off, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1]
@@ -825,7 +890,10 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
     ms_per_step = ms_max / steps
     value = n_total / (ms_per_step / 1e3) / 1e6       # whole-job Mmsgs/s
     wire_gibs = sum_W * world / (ms_per_step / 1e3) / 2**30
-    step_alg = (2 * sum_H + 4 * n) + (0 if wl == "c2" else 2 * sum_W)
+    if args.iov:
+        step_alg = ALG_PER_LAUNCH["iov_len_kernel"](n, sum_W, sum_H) + ALG_PER_LAUNCH["iov_emit_kernel"](n, sum_W, sum_H)
+    else:
+        step_alg = (2 * sum_H + 4 * n) + (0 if wl == "c2" else 2 * sum_W)
     traffic, tsrc = load_traffic(args.traffic_json, wl, n, tm.dom)
     per_gpu = gather_per_gpu(torch, dist, dev, rank, n, tm.ms / steps, tm.ms_clean / steps)
     for r, row in enumerate(per_gpu):
@@ -858,7 +926,11 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
         "validated": ok,
         "wall_s_timed_region": tm.wall_s,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if args.iov:
+        result["config"]["header_bytes_per_gpu"] = sum_H
+        result["config"].pop("parsed_bytes_per_gpu", None)
+        result["config"].pop("decode_mode", None)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.iov:
         prefix = out[: min(total_bytes, 20_000 * 4300)].cpu().numpy().tobytes()
         wire_np = out.cpu().numpy()
         off_np = dec_off.cpu().numpy().view(np.uint64)

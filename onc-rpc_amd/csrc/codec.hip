@@ -465,17 +465,21 @@ int onc_encode_iov(onc_codec* c, const onc_batch* batch, uint8_t* hdr_out, uint6
     a.block_len_base = c->scratch + 3 * T + B;
     a.block_hdr = c->scratch + 2 * T;
     a.block_hdr_base = c->scratch + 2 * T + B;
-    const uint64_t nblk = onc::num_tiles(batch->n);
+    // iov_len workgroup totals (kLenRecs records each); up to kFusedBlocks of
+    // them iov_emit sums itself, beyond that two scan launches place them
+    const uint64_t nblk = onc::num_len_blocks(batch->n);
     rc = run(c, ONC_K_IOV_LEN, "iov_len", [&] { return onc::launch_iov_len(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
-    rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
-        return onc::launch_scan_tiles(a.block_len, a.block_len_base, nblk, 0, nullptr, c->stream);
-    });
-    if (rc != ONC_RC_OK) return rc;
-    rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
-        return onc::launch_scan_tiles(a.block_hdr, a.block_hdr_base, nblk, 0, nullptr, c->stream);
-    });
-    if (rc != ONC_RC_OK) return rc;
+    if (nblk > onc::kFusedBlocks) {
+        rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
+            return onc::launch_scan_tiles(a.block_len, a.block_len_base, nblk, 0, nullptr, c->stream);
+        });
+        if (rc != ONC_RC_OK) return rc;
+        rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
+            return onc::launch_scan_tiles(a.block_hdr, a.block_hdr_base, nblk, 0, nullptr, c->stream);
+        });
+        if (rc != ONC_RC_OK) return rc;
+    }
     return run(c, ONC_K_IOV_EMIT, "iov_emit", [&] { return onc::launch_iov_emit(a, c->stream); });
 }
 

@@ -76,7 +76,7 @@ struct IovArgs {
     int32_t* status;
     uint64_t* totals;          // optional [2]
     uint64_t* tile_sum;        // per 64 records: (wire bytes << 16) | header bytes
-    uint64_t* block_len;       // per 256 records
+    uint64_t* block_len;       // per iov_len workgroup (kLenRecs records)
     uint64_t* block_hdr;
     uint64_t* block_len_base;  // exclusive scans
     uint64_t* block_hdr_base;

@@ -1,0 +1,99 @@
+"""Vectored encode (onc_encode_iov) at iov_len
+workgroup boundaries and beyond the fused-base limit (> 1024 workgroups of
+1024 records: the two scan launches place the workgroups), bit-exact against
+the oracle's contiguous wire (rpc_message.rs:136-164 per record)."""
+import numpy as np
+import pytest
+
+import _onc_pkg
+
+_onc_pkg.load()
+import onc_rpc_amd.layout as L  # noqa: E402
+import onc_rpc_amd.synth as S  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def R():
+    import onc_rpc_amd.runtime as R
+    return R
+
+
+@pytest.fixture(scope="module")
+def codec(R):
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    c = R.Codec(0)
+    yield c
+    c.close()
+
+
+def gpu_iov(R, codec, hb):
+    import torch
+    db = R.DeviceBatch.from_host(hb, "cuda")
+    n = hb.n
+    cap = int(R.codec_lengths(codec, db).sum())
+    hdr = torch.zeros(cap + 16, dtype=torch.uint8, device="cuda")
+    iov = torch.zeros(max(1, n) * 32, dtype=torch.uint8, device="cuda")
+    st = torch.full((max(1, n),), -1, dtype=torch.int32, device="cuda")
+    tot = torch.zeros(2, dtype=torch.int64, device="cuda")
+    codec.encode_iov(db, hdr, iov, st, tot, hdr_cap=cap)
+    codec.sync()
+    return (hdr.cpu().numpy(), iov.cpu().numpy().view(L.IOV_DTYPE)[:n], st.cpu().numpy()[:n],
+            tot.cpu().numpy().view(np.uint64))
+
+
+def reassemble(hb, hdr, iov, st):
+    """The wire writev would send: every accepted record's header slice then
+    its payload slice, vectorised (record order = wire order)."""
+    ok = st == 0
+    e = iov[ok]
+    hl = e["hdr_len"].astype(np.int64)
+    pl = e["payload_len"].astype(np.int64)
+    ho = e["hdr_off"].astype(np.int64)
+    po = e["payload_off"].astype(np.int64)
+    rl = hl + pl
+    start = np.cumsum(rl) - rl
+    out = np.zeros(int(rl.sum()), dtype=np.uint8)
+    # header bytes
+    rh = np.repeat(np.arange(len(e)), hl)
+    k = np.arange(int(hl.sum())) - np.repeat(np.cumsum(hl) - hl, hl)
+    out[start[rh] + k] = hdr[ho[rh] + k]
+    # payload bytes, in place in the caller's arena
+    rp = np.repeat(np.arange(len(e)), pl)
+    j = np.arange(int(pl.sum())) - np.repeat(np.cumsum(pl) - pl, pl)
+    out[start[rp] + hl[rp] + j] = hb.payload_arena[po[rp] + j]
+    return out, start
+
+
+def check(hb, oracle, hdr, iov, st, tot):
+    o_wire, o_off, o_st, _ = oracle.encode_batch(hb)
+    assert np.array_equal(st, o_st)
+    ok = st == 0
+    got, start = reassemble(hb, hdr, iov, st)
+    assert got.tobytes() == bytes(o_wire)
+    assert np.array_equal(iov["wire_off"][ok], o_off[:-1][ok])
+    assert np.array_equal(start, o_off[:-1][ok].astype(np.int64))
+    hl = iov["hdr_len"].astype(np.uint64)
+    assert np.array_equal(iov["hdr_off"][ok], (np.cumsum(hl) - hl)[ok])
+    assert int(tot[0]) == int(hl.sum()) and int(tot[1]) == len(o_wire)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1023, 1024, 1025, 4095, 4097, 16385, 70001])
+def test_iov_workgroup_boundaries(codec, R, oracle, n):
+    hb = S.mixed(n, seed=100 + n % 97, pmin=0, pmax=300, exotic=0.2)
+    check(hb, oracle, *gpu_iov(R, codec, hb))
+
+
+def test_iov_auth_unix_tiles(codec, R, oracle):
+    # 32-word headers (the padded LDS staging) and odd payloads
+    hb = S.call_unix16(5000, 1023)
+    check(hb, oracle, *gpu_iov(R, codec, hb))
+
+
+def test_iov_beyond_fused_blocks(codec, R, oracle):
+    # 1075 iov_len workgroups > kFusedBlocks (1024): the scan-launch placement
+    n = 1_100_000
+    hb = S.mixed(n, seed=9, pmin=0, pmax=64, exotic=0.1)
+    check(hb, oracle, *gpu_iov(R, codec, hb))
