@@ -69,6 +69,9 @@ def parse(argv=None):
     ap.add_argument("--iov", action="store_true",
                     help="c0/c1/c3: the step is the vectored encode (onc_encode_iov: packed headers + one iovec "
                          "per record, payloads referenced in place) instead of encode + decode")
+    ap.add_argument("--iov-leg", choices=["on", "off"], default="on",
+                    help="with the c1 workload: also run the vectored encode of the same configs[1] batch and report "
+                         "it as `vectored_encode`")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend of the ranks (control plane only)")
     ap.add_argument("--check-launch", action="store_true",
                     help="start the ranks, check the world size and print it; no GPU work (launcher test)")
@@ -992,6 +995,17 @@ def main():
     else:
         result = run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode)
         ok = result["validated"]
+        if args.workload == "c1" and not args.iov and args.iov_leg == "on":
+            import copy
+            la = copy.copy(args)
+            la.iov, la.no_pcie, la.no_cpu_baseline = True, True, True
+            leg = run_main(la, torch, R, S, SH, L, dist, rank, world, local_rank, mode)
+            ok = ok and leg["validated"]
+            result["vectored_encode"] = {k: leg[k] for k in ("value", "unit", "ms_per_step", "validated", "data",
+                                                             "roofline", "kernels_breakdown_pass")}
+            result["vectored_encode"]["note"] = ("onc_encode_iov (SURVEY §8(f) rank 2) of the same configs[1] "
+                                                 "batch: packed headers + 32-byte iovecs, payloads in place; "
+                                                 "checked byte for byte against the contiguous encode")
         if args.c4_leg == "on":
             result["configs4"] = run_c4(args, torch, R, S, SH, L, dist, rank, world, local_rank,
                                         args.c4_records, mode, args.steps, args.warmup)

@@ -8,7 +8,7 @@ OUT=$PWD/gpurun_out
 for wl in ${WORKLOADS:-c1 c2 c3 c0}; do
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --kernel-trace --pmc $ctr -d $OUT/pmc_${wl}_$ctr -o run --output-format csv -- \
-        python3 bench.py --workload $wl --steps 3 --warmup 1 --no-cpu-baseline --no-pcie > $OUT/pmc_${wl}_$ctr.log 2>&1
+        python3 bench.py --workload $wl --steps 3 --warmup 1 --no-cpu-baseline --no-pcie --c4-leg off > $OUT/pmc_${wl}_$ctr.log 2>&1
     rc=$?; echo "pmc $wl $ctr rc=$rc"
     [ $rc -eq 0 ] || exit $rc
   done
