@@ -704,7 +704,7 @@ def validate_iov(torch, n, iov, hdr_out, iov_tot, iov_status, wire, rec_off, hdr
     if int((iov_status[:n] != 0).sum()) or int(iov_tot[0]) != hdr_total or int(iov_tot[1]) != total_bytes:
         return False
     e = iov[: 32 * n].view(torch.int64).view(n, 4)
-    hoff, poff, woff = e[:, 0], e[:, 1], e[:, 2]
+    hoff, poff, woff = e[:, 0].contiguous(), e[:, 1], e[:, 2].contiguous()
     hl = e[:, 3] & 0xFFFFFFFF
     pl = (e[:, 3] >> 32) & 0xFFFFFFFF
     if not torch.equal(woff, rec_off[:n]) or not torch.equal(hl, hdr_len_ref) or not torch.equal(pl, plen):
