@@ -97,3 +97,30 @@ def test_iov_beyond_fused_blocks(codec, R, oracle):
     n = 1_100_000
     hb = S.mixed(n, seed=9, pmin=0, pmax=64, exotic=0.1)
     check(hb, oracle, *gpu_iov(R, codec, hb))
+
+
+def _max_unix(name_len, ngids, rng):
+    return {"kind": "unix", "stamp": int(rng.integers(0, 2**32)), "machine_name": rng.bytes(name_len).hex(),
+            "uid": int(rng.integers(0, 2**32)), "gid": int(rng.integers(0, 2**32)),
+            "gids": [int(x) for x in rng.integers(0, 2**32, ngids)]}
+
+
+def test_iov_maximal_headers(codec, R, oracle):
+    """Tiles of 460-byte headers (credential and verifier both AUTH_UNIX at
+    the associated-data limit, flavor.rs:110): 29 KiB of headers per tile,
+    past the LDS staging budget, so those records write their own words;
+    interleaved with ordinary tiles staged in LDS."""
+    rng = np.random.default_rng(5)
+    msgs = []
+    for i in range(64 * 12):
+        big = (i // 64) % 2 == 0
+        if big:
+            c = [(124, 16), (188, 0)][int(rng.integers(0, 2))]
+            v = [(124, 16), (188, 0)][int(rng.integers(0, 2))]
+            cred, verf = _max_unix(*c, rng), _max_unix(*v, rng)
+        else:
+            cred, verf = {"kind": "none"}, {"kind": "none"}
+        msgs.append({"xid": i, "type": "call", "program": 1, "program_version": 2, "procedure": 3,
+                     "cred": cred, "verf": verf, "payload": rng.bytes(int(rng.integers(0, 40))).hex()})
+    hb = L.build_batch(msgs)
+    check(hb, oracle, *gpu_iov(R, codec, hb))
