@@ -264,9 +264,12 @@ int onc_abi_version(void);
  * keeps the event overhead off the other launches. An id names a launch
  * site: ONC_K_ENC_EMIT is either enc_emit kernel; ONC_K_LEN_TILES /
  * ONC_K_LEN_APPLY are onc_scan_lengths' first and second launch (lenblk /
- * lenoff up to 8M records); ONC_K_FRAME_COUNTS / ONC_K_FRAME_OFFSETS the
- * framer's count scan (frame_cblk / frame_coff, or frame_counts and the
- * three-launch scan beyond 512k chunks). */
+ * lenoff up to 8M records); ONC_K_FRAME_COUNTS the framer's count pass
+ * (frame_cblk, or frame_counts ahead of the three-launch scan beyond 512k
+ * chunks); ONC_K_FRAME_WRITE its start copy, which up to 512k chunks also
+ * sums each chunk's first record index. ONC_K_FRAME_OFFSETS keeps its
+ * number but no launch carries it any more (its offsets pass, frame_coff,
+ * is folded into the start copy). */
 #define ONC_K_ENC_LEN      0
 #define ONC_K_SCAN_TILES   1
 #define ONC_K_ENC_EMIT     2

@@ -548,13 +548,12 @@ int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* 
     rc = run(c, ONC_K_FRAME_WALK, "frame_walk", [&] { return onc::launch_frame_walk(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
     if (onc::frame_fused_scan_ok(P) && !c->force_scan) {
-        // counts + block totals, per-block bases + chunk scan, then a wave per
-        // chunk copying its kept record starts
+        // counts + block totals, then a wave per chunk summing its first
+        // record index and copying its kept record starts
         rc = run(c, ONC_K_FRAME_COUNTS, "frame_cblk", [&] { return onc::launch_frame_cblk(a, tile_sum, c->stream); });
         if (rc != ONC_RC_OK) return rc;
-        rc = run(c, ONC_K_FRAME_OFFSETS, "frame_coff", [&] { return onc::launch_frame_coff(a, tile_sum, c->stream); });
-        if (rc != ONC_RC_OK) return rc;
-        return run(c, ONC_K_FRAME_WRITE, "frame_write", [&] { return onc::launch_frame_write_slots(a, c->stream); });
+        return run(c, ONC_K_FRAME_WRITE, "frame_write",
+                   [&] { return onc::launch_frame_write_slots(a, tile_sum, c->stream); });
     }
     rc = run(c, ONC_K_FRAME_COUNTS, "frame_counts", [&] { return onc::launch_frame_counts(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;

@@ -416,8 +416,8 @@ __global__ __launch_bounds__(64) void frame_walk_kernel(FrameArgs a) {
 // Records of chunk t that belong to the framed stream, summed per block of
 // kCntBlk chunks (one per thread: a 2 GB stream is only 30k chunks, so the
 // grid stays wide): the counts kernel and the first level of the count scan
-// in one launch. frame_coff then gives every chunk its first record index
-// (each block sums the block totals before it itself).
+// in one launch. frame_write_slots then sums every chunk's first record
+// index itself (the block totals before its block + the counts before it).
 constexpr uint64_t kCntBlk = 256;
 constexpr uint64_t kCntBlkMax = 2048;   // 512k chunks (32 GiB of stream at 64 KiB); beyond: the 3-launch scan
 
@@ -434,23 +434,6 @@ __global__ __launch_bounds__(256) void frame_cblk_kernel(FrameArgs a, uint64_t* 
     uint64_t total;
     block_excl_scan_u64<256>(ce, s_wave, &total);
     if (threadIdx.x == 0) blk_sum[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(256) void frame_coff_kernel(FrameArgs a, const uint64_t* blk_sum) {
-    __shared__ uint64_t s_wave[4];
-    const uint64_t b = blockIdx.x;
-    const uint64_t t = b * kCntBlk + threadIdx.x;
-    const uint32_t v = t < a.nchunks ? a.cnt_eff[t] : 0u;
-    uint64_t pre = 0;
-#pragma unroll
-    for (int k = 0; k < int(kCntBlkMax / 256); ++k) {
-        const uint64_t j = uint64_t(threadIdx.x) + uint64_t(k) * 256;
-        if (j < b) pre += blk_sum[j];
-    }
-    uint64_t pre_total, total;
-    block_excl_scan_u64<256>(pre, s_wave, &pre_total);
-    const uint64_t run = pre_total + block_excl_scan_u64<256>(v, s_wave, &total);
-    if (t < a.nchunks) a.cnt_base[t] = run;
 }
 
 // Records of chunk t that belong to the framed stream.
@@ -474,12 +457,27 @@ __device__ __forceinline__ void put_result(const FrameArgs& a, uint64_t n, uint6
 // rec_off from the kept starts: a wave per chunk, lane i copies the chunk's
 // record i (coalesced 8-byte stores of consecutive records); a chunk with
 // more than kStartsCap records is re-chased by its lane 0 (small records).
-__global__ __launch_bounds__(256) void frame_write_slots_kernel(FrameArgs a) {
+// The chunk's first record index is the sum of the block totals before its
+// block and of the counts before it in its block (frame_cblk's outputs, L2
+// hits, one round trip): no separate offsets launch.
+__global__ __launch_bounds__(256) void frame_write_slots_kernel(FrameArgs a, const uint64_t* blk_sum) {
     const uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
     const uint32_t i = threadIdx.x & 63;
     if (t >= a.nchunks) return;
+    const uint64_t b = t / kCntBlk;
+    const uint64_t u0 = b * kCntBlk;
+    uint32_t cc[kCntBlk / 64];
+#pragma unroll
+    for (int q = 0; q < int(kCntBlk / 64); ++q) {
+        const uint64_t u = u0 + i + 64ull * q;
+        cc[q] = u < t ? a.cnt_eff[u] : 0u;
+    }
     const uint32_t ce = a.cnt_eff[t];
-    const uint64_t k0 = a.cnt_base[t];
+    uint64_t s = 0;
+    for (uint64_t j = i; j < b; j += 64) s += blk_sum[j];
+#pragma unroll
+    for (int q = 0; q < int(kCntBlk / 64); ++q) s += cc[q];
+    const uint64_t k0 = lane_u64(wave_incl_scan_u64(s), 63);
     if (ce != 0 && k0 <= a.max_records) {
         const uint64_t* rec = a.starts + t * kStartsCap;
         if (ce <= kStartsCap) {
@@ -566,14 +564,8 @@ hipError_t launch_frame_cblk(const FrameArgs& a, uint64_t* blk_sum, hipStream_t 
     return hipGetLastError();
 }
 
-hipError_t launch_frame_coff(const FrameArgs& a, const uint64_t* blk_sum, hipStream_t s) {
-    ONC_LAUNCH(frame_coff_kernel, dim3(uint32_t((a.nchunks + kCntBlk - 1) / kCntBlk)), dim3(256), 0, s, a,
-                       blk_sum);
-    return hipGetLastError();
-}
-
-hipError_t launch_frame_write_slots(const FrameArgs& a, hipStream_t s) {
-    ONC_LAUNCH(frame_write_slots_kernel, dim3(uint32_t((a.nchunks + 3) / 4)), dim3(256), 0, s, a);
+hipError_t launch_frame_write_slots(const FrameArgs& a, const uint64_t* blk_sum, hipStream_t s) {
+    ONC_LAUNCH(frame_write_slots_kernel, dim3(uint32_t((a.nchunks + 3) / 4)), dim3(256), 0, s, a, blk_sum);
     return hipGetLastError();
 }
 

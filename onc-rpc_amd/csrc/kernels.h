@@ -143,8 +143,7 @@ hipError_t launch_frame_chunks(const FrameArgs& a, hipStream_t s);
 hipError_t launch_frame_write(const FrameArgs& a, hipStream_t s);
 bool frame_fused_scan_ok(uint64_t nchunks);
 hipError_t launch_frame_cblk(const FrameArgs& a, uint64_t* blk_sum, hipStream_t s);
-hipError_t launch_frame_coff(const FrameArgs& a, const uint64_t* blk_sum, hipStream_t s);
-hipError_t launch_frame_write_slots(const FrameArgs& a, hipStream_t s);
+hipError_t launch_frame_write_slots(const FrameArgs& a, const uint64_t* blk_sum, hipStream_t s);
 // scan.hip
 hipError_t launch_scan_tiles(const uint64_t* in, uint64_t* out_excl, uint64_t count, uint64_t base,
                              uint64_t* total_out, hipStream_t s);
