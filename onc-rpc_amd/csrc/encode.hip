@@ -891,6 +891,9 @@ __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
 // finds them cached, made the decode slower: 60 -> 69 us on c1, the dirty
 // lines are written back at the kernel boundary);
 // kOcc: workgroups per CU the register allocation must allow (0 = free)
+#ifndef ONC_EMIT_OCC
+#define ONC_EMIT_OCC 0   // lab: waves per SIMD the wave-per-tile kernel's registers must allow (0 = free: 106 VGPRs, 4)
+#endif
 template <int kU, int kNT = 0, int kOcc = 0, bool kFused = false, int kPipe = 2>
 __global__ __launch_bounds__(64 * kFastWaves, kOcc ? kOcc * kFastWaves / 4 : 1) void enc_emit_kernel_t(EncArgs a) {
     __shared__ ImgTile s_tiles[kFastWaves];
@@ -914,10 +917,10 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
     }
     const uint64_t blocks = (num_emit_tiles(a.n) + kFastWaves - 1) / kFastWaves;
     if (a.fused_base)
-        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, true>), dim3(uint32_t(blocks)),
+        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, ONC_EMIT_OCC, true>), dim3(uint32_t(blocks)),
                            dim3(64 * kFastWaves), 0, s, a);
     else
-        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, false>), dim3(uint32_t(blocks)),
+        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, ONC_EMIT_OCC, false>), dim3(uint32_t(blocks)),
                            dim3(64 * kFastWaves), 0, s, a);
     return hipGetLastError();
 }
