@@ -239,11 +239,23 @@ struct ImgSink {
 
 // One chunk of the word path: dword i is payload (sel bit i) taken from the
 // rotated load, else the image dword.
+// The rotation by `rot` dwords is two select stages on its bits (8 selects)
+// rather than a 4-way select per dword.
 __device__ __forceinline__ void merge_words(const u32x4_a4& X, const uint4& L, uint32_t sel, uint32_t v[4]) {
+#ifdef ONC_MERGE_SEL4
     const uint32_t rot = sel >> 4;
     const uint32_t h[4] = {L.x, L.y, L.z, L.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = (sel >> i) & 1 ? sel4(X, (i + rot) & 3) : h[i];
+#else
+    const bool r1 = (sel >> 4) & 1u, r2 = (sel >> 5) & 1u;
+    const uint32_t a0 = r1 ? X.y : X.x, a1 = r1 ? X.z : X.y, a2 = r1 ? X.w : X.z, a3 = r1 ? X.x : X.w;
+    const uint32_t z0 = r2 ? a2 : a0, z1 = r2 ? a3 : a1, z2 = r2 ? a0 : a2, z3 = r2 ? a1 : a3;
+    v[0] = sel & 1u ? z0 : L.x;
+    v[1] = sel & 2u ? z1 : L.y;
+    v[2] = sel & 4u ? z2 : L.z;
+    v[3] = sel & 8u ? z3 : L.w;
+#endif
 }
 
 // One chunk of the byte path: bytes [lo, hi) of the chunk are payload, taken
@@ -298,9 +310,16 @@ __device__ __forceinline__ ChunkPlan plan_chunk(const ImgTile& T, uint32_t gsh, 
         const uint32_t hi = hasp ? min(q.y - o, 16u) : 0u;
         P.sel = ((o - x) & 15u) | (lo << 8) | (hi << 16);
     } else {
+#ifdef ONC_MERGE_SEL4
         uint32_t pm = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) pm |= (o + 4 * i >= q.x && o + 4 * i < q.y) ? (1u << i) : 0u;
+#else
+        // dwords i with o + 4i in [q.x, q.y) (word path: q.x, q.y, o all 4-aligned)
+        const uint32_t lo = min(max(int32_t(q.x - o), 0), 16) >> 2;
+        const uint32_t hi = min(max(int32_t(q.y - o), 0), 16) >> 2;
+        const uint32_t pm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+#endif
         P.sel = (hasp ? pm : 0u) | (((o - x) >> 2) & 3u) << 4;
     }
     return P;
