@@ -58,6 +58,26 @@ struct Rd {
         }
         return bswap(load4(base + pos));
     }
+
+    // n (<= 16) consecutive words from record position pos into out[0..n),
+    // zeros after: straight from the window (17 LDS reads at fixed offsets,
+    // each word's bytes funnelled from two neighbours) when all of them lie
+    // in it, else word by word.
+    __device__ __forceinline__ void words16(uint32_t pos, uint32_t n, uint32_t out[ONC_MAX_GIDS]) const {
+        const uint32_t q = q0 + pos;
+        if (q + 4u * n <= lim) {
+            const uint32_t sh = q & 3u;
+            const uint32_t* p = col + (q >> 2) * kDecTile;
+            uint32_t w[ONC_MAX_GIDS + 1];
+#pragma unroll
+            for (uint32_t k = 0; k <= ONC_MAX_GIDS; ++k) w[k] = (k < n || (k == n && sh)) ? p[k * kDecTile] : 0u;
+#pragma unroll
+            for (uint32_t g = 0; g < ONC_MAX_GIDS; ++g) out[g] = g < n ? bswap(funnel(w[g], w[g + 1], sh)) : 0u;
+        } else {
+#pragma unroll
+            for (uint32_t g = 0; g < ONC_MAX_GIDS; ++g) out[g] = g < n ? be32(pos + 4u * g) : 0u;
+        }
+    }
 };
 
 #define ONC_RD(var)                                   \
@@ -187,13 +207,12 @@ __device__ __forceinline__ int32_t auth_slice(const Rd& R, uint32_t& pos, uint32
         ONC_RD(gid);
         ONC_RD(ng);
         if (ng > ONC_MAX_GIDS) return ONC_ERR_INVALID_AUTH_DATA;          // unix_params.rs:112
+        // the gids: every short read among them is the same error, so one
+        // bounds check stands for the reference's per-gid reads
+        if (uint64_t(pos) + 4ull * ng > end) return kShort;
         uint32_t gids[ONC_MAX_GIDS];
-#pragma unroll
-        for (uint32_t g = 0; g < ONC_MAX_GIDS; ++g) {
-            uint32_t v = 0;
-            if (g < ng) ONC_RD(v);
-            gids[g] = v;
-        }
+        R.words16(pos, ng, gids);
+        pos += 4u * ng;
         if (pos - start != n) return ONC_ERR_INVALID_AUTH_DATA;          // unix_params.rs:117-119
         put_unix(us, slot, stamp, uid, gid, ng, rec_off + name_pos, nl, gids);
         a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
@@ -244,13 +263,10 @@ __device__ __forceinline__ int32_t auth_bytes(const Rd& R, uint32_t& pos, uint32
         ONC_RDQ(gid);
         ONC_RDQ(ng);
         if (ng > ONC_MAX_GIDS) return ONC_ERR_INVALID_AUTH_DATA;
+        if (uint64_t(q) + 4ull * ng > bend) return ONC_ERR_INVALID_LENGTH;   // every gid's try_u32 fails alike
         uint32_t gids[ONC_MAX_GIDS];
-#pragma unroll
-        for (uint32_t g = 0; g < ONC_MAX_GIDS; ++g) {
-            uint32_t v = 0;
-            if (g < ng) ONC_RDQ(v);
-            gids[g] = v;
-        }
+        R.words16(q, ng, gids);
+        q += 4u * ng;
 #undef ONC_RDQ
         // params.serialised_len() != auth_data.len() -> InvalidAuthData (flavor.rs:204-208)
         if (20u + nl + pad4(nl) + 4u * ng != n) return ONC_ERR_INVALID_AUTH_DATA;
