@@ -325,6 +325,38 @@ __device__ __forceinline__ ChunkPlan plan_chunk(const ImgTile& T, uint32_t gsh, 
     return P;
 }
 
+// Word path, interior span (every payload's 16-byte-granular source window
+// lies inside the payload arena; the producer checks it per span): the load
+// for chunk c is taken at the unclamped source of its own bytes, so the
+// loaded dwords are already in place — no rotation, and bytes outside the
+// record's payload are other arena bytes, replaced by the image's.
+__device__ __forceinline__ ChunkPlan plan_chunk_interior(const ImgTile& T, uint32_t gsh, uint64_t B0, int32_t c,
+                                                         uintptr_t dummy) {
+    int r = T.map[c >> gsh];
+    if (gsh != 0)
+        while (c >= T.ent[r + 1].x) ++r;
+    const int4 m = T.ent[r];
+    const uint4 q = T.pay[r];
+    const int32_t s = c - m.w - (c >= m.z ? m.z - m.y : 0);
+    ChunkPlan P;
+    P.slot = s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s);
+    const uint32_t o = uint32_t(c) << 4;
+    const bool hasp = q.x < q.y && o < q.y && o + 16 > q.x;
+    const uint64_t sbase = uint64_t(q.z) | (uint64_t(q.w) << 32);
+    P.A = hasp ? sbase + B0 + o : dummy;
+    const uint32_t lo = min(max(int32_t(q.x - o), 0), 16) >> 2;
+    const uint32_t hi = min(max(int32_t(q.y - o), 0), 16) >> 2;
+    P.sel = hasp ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+    return P;
+}
+
+__device__ __forceinline__ void merge_words_inplace(const uint32_t X[4], const uint4& L, uint32_t sel, uint32_t v[4]) {
+    v[0] = sel & 1u ? X[0] : L.x;
+    v[1] = sel & 2u ? X[1] : L.y;
+    v[2] = sel & 4u ? X[2] : L.z;
+    v[3] = sel & 8u ? X[3] : L.w;
+}
+
 template <int kNT, bool kByte>
 __device__ __forceinline__ void load_chunk(const ChunkPlan& P, uint32_t X[4]) {
     if (kByte) {
@@ -592,6 +624,7 @@ struct SpanHdr {
     uint32_t gsh;
     uint32_t byte_mode;
     uint32_t state;          // 0: nothing to stream, 1: stream, 2: no more spans
+    uint32_t interior;       // word path: every payload source window inside the arena (plan_chunk_interior)
 };
 struct WsSlot {
     ImgTile T;
@@ -742,6 +775,14 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
             for (int32_t g = (own_lo + (1 << gsh) - 1) >> gsh; g < g_hi; ++g) W.T.map[g] = uint8_t(j);
         }
     }
+    // interior: the 16-byte-granular source windows of every payload of the
+    // span (from its first to its last output chunk) lie inside the arena
+    bool inside = true;
+    if (active && Splen >= 16) {
+        const uint64_t head = Spst & 15u, tail = (16u - (Sen & 15u)) & 15u;
+        inside = Spoff >= head && Spoff + Splen + tail <= a.bounds.payload_len;
+    }
+    const bool interior = __all(inside);
     const uint64_t E = min(S1, a.out_cap);
     if (lane == 0) {
         W.T.ent[hi_rec - lo_rec] = make_int4(0x7FFFFFFF, 0, 0, 0);
@@ -753,6 +794,7 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
         h.gsh = gsh;
         h.byte_mode = S.byte_mode ? 1u : 0u;
         h.state = E > S0 ? 1u : 0u;
+        h.interior = interior && !S.byte_mode ? 1u : 0u;
         W.h = h;
     }
     S.lo_rec = hi_rec;
@@ -762,7 +804,7 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
 // steps of 64 * kU chunks, this wave taking steps part, part + nparts, ...
 // (same two-register-set pipeline); part 0 also writes the partial edge
 // chunks.
-template <int kU, int kNT, bool kByte>
+template <int kU, int kNT, bool kByte, bool kInterior = false>
 __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile& T, const SpanHdr& h, int part,
                                                  int nparts, uintptr_t dummy) {
     const int lane = threadIdx.x & 63;
@@ -779,7 +821,9 @@ __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile
         uint4 La[kU], Lb[kU];
 #define ONC_ISSUE(P, X, L, base)                                                          \
     _Pragma("unroll") for (int u = 0; u < kU; ++u) {                                     \
-        P[u] = plan_chunk<kByte>(T, gsh, B0, min((base) + lane + 64 * u, cl - 1), dummy);   \
+        const int32_t c_ = min((base) + lane + 64 * u, cl - 1);                           \
+        P[u] = kInterior ? plan_chunk_interior(T, gsh, B0, c_, dummy)                     \
+                         : plan_chunk<kByte>(T, gsh, B0, c_, dummy);                      \
         load_chunk<kNT, kByte>(P[u], X[u]);                                               \
         L[u] = T.img[P[u].slot];                                                          \
     }
@@ -787,7 +831,8 @@ __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile
     _Pragma("unroll") for (int u = 0; u < kU; ++u) {                                     \
         const int32_t c = min((base) + lane + 64 * u, cl - 1);                            \
         uint32_t v[4];                                                                    \
-        merge_chunk<kByte>(P[u], X[u], L[u], v);                                          \
+        if (kInterior) merge_words_inplace(X[u], L[u], P[u].sel, v);                      \
+        else merge_chunk<kByte>(P[u], X[u], L[u], v);                                     \
         u32x4* d = reinterpret_cast<u32x4*>(a.out + B0 + (uint64_t(c) << 4));             \
         if (kNT & 2) __builtin_nontemporal_store(u32x4{v[0], v[1], v[2], v[3]}, d);        \
         else *d = u32x4{v[0], v[1], v[2], v[3]};                                          \
@@ -879,6 +924,8 @@ __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
         } else if (state == 1u) {
             const SpanHdr h = s_slot[cur].h;
             if (h.byte_mode) stream_span_part<1, kNT, true>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
+            else if (h.interior && !(a.variant & 0x4000))
+                stream_span_part<kU, kNT, false, true>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
             else stream_span_part<kU, kNT, false>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
         }
 #ifdef ONC_EMIT_PROF
