@@ -203,10 +203,14 @@ constexpr uint64_t kSpanBytesMax = 1ull << 30;  // a span's offsets fit uint32 (
 // only static requirement is that one maximal record always fits on its own.
 static_assert((4 * (7 + 2 * 54) + 15 + 15) / 16 + 1 <= kImgChunks, "one maximal record must fit the image");
 
+// pay[].x = pay[].y of a record with no streamed payload (none, or under 16
+// bytes and kept in the image): no chunk overlaps [kNoPay, kNoPay)
+constexpr uint32_t kNoPay = 0x7FFFFFF0u;
+
 struct ImgTile {
     uint4 img[kImgChunks];           // assembled non-pure chunks (header bytes; small payloads)
-    int4 ent[kEmitRecs + 1];         // {cf, cp0, cp1, NP} (chunks, span-relative); [ns].x = sentinel
-    uint4 pay[kEmitRecs + 1];        // {pst, en (bytes, span-chunk-relative; pst = en: no stream payload), src lo, hi}
+    int4 ent[kEmitRecs + 1];         // {cf, NP + pure chunks, cp1, NP} (chunks, span-relative); [ns].x = sentinel
+    uint4 pay[kEmitRecs + 1];        // {pst, en (bytes, span-chunk-relative; kNoPay both: no stream payload), src lo, hi}
     uint8_t map[kMap2Cap];           // granule -> span record owning its first chunk
 };
 
@@ -297,7 +301,7 @@ __device__ __forceinline__ ChunkPlan plan_chunk(const ImgTile& T, uint32_t gsh, 
         while (c >= T.ent[r + 1].x) ++r;
     const int4 m = T.ent[r];
     const uint4 q = T.pay[r];
-    const int32_t s = c - m.w - (c >= m.z ? m.z - m.y : 0);
+    const int32_t s = c - (c >= m.z ? m.y : m.w);     // image slot: NP before the pure run, NP + its length after
     ChunkPlan P;
     P.slot = s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s);
     const uint32_t o = uint32_t(c) << 4;
@@ -337,16 +341,16 @@ __device__ __forceinline__ ChunkPlan plan_chunk_interior(const ImgTile& T, uint3
         while (c >= T.ent[r + 1].x) ++r;
     const int4 m = T.ent[r];
     const uint4 q = T.pay[r];
-    const int32_t s = c - m.w - (c >= m.z ? m.z - m.y : 0);
+    const int32_t s = c - (c >= m.z ? m.y : m.w);     // image slot: NP before the pure run, NP + its length after
     ChunkPlan P;
     P.slot = s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s);
     const uint32_t o = uint32_t(c) << 4;
-    const bool hasp = q.x < q.y && o < q.y && o + 16 > q.x;
+    const bool hasp = o < q.y && o + 16 > q.x;          // kNoPay records: never
     const uint64_t sbase = uint64_t(q.z) | (uint64_t(q.w) << 32);
     P.A = hasp ? sbase + B0 + o : dummy;
     const uint32_t lo = min(max(int32_t(q.x - o), 0), 16) >> 2;
     const uint32_t hi = min(max(int32_t(q.y - o), 0), 16) >> 2;
-    P.sel = hasp ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+    P.sel = hasp ? ((1u << (hi - lo)) - 1u) << lo : 0u;
     return P;
 }
 
@@ -560,9 +564,10 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         if (active) {
             const bool small = plen != 0 && plen < 16;    // payload kept in the image
             const uintptr_t sb = payload + poff - pst;    // payload byte at output offset o: sb + o
-            T.ent[j] = make_int4(int32_t(cfa - C0), int32_t(p0 - C0), int32_t(p1 - C0), int32_t(NP));
+            T.ent[j] = make_int4(int32_t(cfa - C0), int32_t(NP + npx), int32_t(p1 - C0), int32_t(NP));
             const uint32_t ps = uint32_t(pst - B0), pe = uint32_t(en - B0);
-            T.pay[j] = make_uint4(small ? pe : ps, pe, uint32_t(sb), uint32_t(sb >> 32));
+            const bool nopay = small || ps == pe;
+            T.pay[j] = make_uint4(nopay ? kNoPay : ps, nopay ? kNoPay : pe, uint32_t(sb), uint32_t(sb >> 32));
             if (len != 0) {
                 // the record's non-pure bytes are contiguous in the image from
                 // image byte start - 16 (C0 + NP)
@@ -753,9 +758,10 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
     if (active) {
         const bool small = Splen != 0 && Splen < 16;
         const uintptr_t sb = payload + Spoff - Spst;
-        W.T.ent[j] = make_int4(int32_t(Scfa - C0), int32_t(Sp0 - C0), int32_t(Sp1 - C0), int32_t(NP));
+        W.T.ent[j] = make_int4(int32_t(Scfa - C0), int32_t(NP + npx), int32_t(Sp1 - C0), int32_t(NP));
         const uint32_t ps = uint32_t(Spst - B0), pe = uint32_t(Sen - B0);
-        W.T.pay[j] = make_uint4(small ? pe : ps, pe, uint32_t(sb), uint32_t(sb >> 32));
+        const bool nopay = small || ps == pe;
+        W.T.pay[j] = make_uint4(nopay ? kNoPay : ps, nopay ? kNoPay : pe, uint32_t(sb), uint32_t(sb >> 32));
         if (Slen != 0) {
             const uint64_t ibb = Sstart - 16ull * uint64_t(C0 + NP);
             MsgRegs mr2 = issue_msg(a.msgs + S.r0 + lane);
