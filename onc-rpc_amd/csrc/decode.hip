@@ -41,19 +41,24 @@ constexpr int kDecTile = ONC_DEC_TILE;
 #define ONC_DEC_STAGE_MIN 32   // AUTH_UNIX records in a workgroup from which its slots are staged
 #endif        // records (lanes) per decode workgroup
 
+// The window column holds the record's words dword-aligned to the record:
+// column word k = record bytes [4k - sh, 4k - sh + 4) (the loaded 16-byte
+// granules stored shifted by the record's dword offset in its first
+// granule), so record word k is column word k when the record starts on a
+// 4-byte boundary and a funnel of words k and k + 1 otherwise — fields at
+// fixed record positions read at fixed LDS offsets.
 struct Rd {
     uintptr_t base;          // absolute address of record byte 0
-    uint32_t q0;             // window offset of record byte 0 (0..15)
-    uint32_t lim;            // window bytes loaded
+    uint32_t sh;             // record byte 0's offset in its dword (0..3)
+    uint32_t lim;            // record bytes held by the window
     const uint32_t* col;     // this lane's window column (stride kDecTile words)
 
-    // Big-endian u32 at record-relative position pos (all 4 bytes valid).
+    // Big-endian u32 at record-relative position pos (pos % 4 == 0; all 4 bytes valid).
     __device__ __forceinline__ uint32_t be32(uint32_t pos) const {
-        const uint32_t q = q0 + pos;
-        if (q + 4u <= lim) {
-            const uint32_t wi = q >> 2, sh = q & 3u;
-            const uint32_t w0 = col[wi * kDecTile];
-            const uint32_t w1 = sh ? col[(wi + 1) * kDecTile] : 0u;
+        if (pos + 4u <= lim) {
+            const uint32_t k = pos >> 2;
+            const uint32_t w0 = col[k * kDecTile];
+            const uint32_t w1 = sh ? col[(k + 1) * kDecTile] : 0u;
             return bswap(funnel(w0, w1, sh));
         }
         return bswap(load4(base + pos));
@@ -64,10 +69,8 @@ struct Rd {
     // each word's bytes funnelled from two neighbours) when all of them lie
     // in it, else word by word.
     __device__ __forceinline__ void words16(uint32_t pos, uint32_t n, uint32_t out[ONC_MAX_GIDS]) const {
-        const uint32_t q = q0 + pos;
-        if (q + 4u * n <= lim) {
-            const uint32_t sh = q & 3u;
-            const uint32_t* p = col + (q >> 2) * kDecTile;
+        if (pos + 4u * n <= lim) {
+            const uint32_t* p = col + (pos >> 2) * kDecTile;
             uint32_t w[ONC_MAX_GIDS + 1];
 #pragma unroll
             for (uint32_t k = 0; k <= ONC_MAX_GIDS; ++k) w[k] = (k < n || (k == n && sh)) ? p[k * kDecTile] : 0u;
@@ -453,6 +456,7 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     const uintptr_t base = wire + b;
     const uintptr_t win = base & ~uintptr_t(15);
     const uint32_t q0 = uint32_t(base - win);
+    const uint32_t d0 = q0 >> 2;                      // record byte 0's dword in its first granule
     // Stage the window. Chunks past the record's last byte are not loaded;
     // empty records read nothing.
     uint32_t nch = 0;
@@ -464,20 +468,21 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
 #pragma unroll
         for (uint32_t j = 0; j < kWin1; ++j)
             if (j < nch) v[j] = gload<u32x4>(win + 16 * j);
+        // stored shifted by d0 dwords: column word 0 holds record byte 0's dword
 #pragma unroll
         for (uint32_t j = 0; j < kWin1; ++j) {
             if (j < nch) {
-                s_win[(4 * j + 0) * kDecTile + t] = v[j].x;
-                s_win[(4 * j + 1) * kDecTile + t] = v[j].y;
-                s_win[(4 * j + 2) * kDecTile + t] = v[j].z;
-                s_win[(4 * j + 3) * kDecTile + t] = v[j].w;
+                const uint32_t e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k)
+                    if (4 * j + k >= d0) s_win[(4 * j + k - d0) * kDecTile + t] = e[k];
             }
         }
         // Header extent from the first round: call -> 36 + cred body + verf
         // flavor/length + the verifier body (its length when the first round
         // holds it, else a 16-byte guess); reply -> up to 12 bytes past an
         // accepted verifier.
-        const Rd R1{base, q0, 16 * nch, &s_win[t]};
+        const Rd R1{base, q0 & 3u, 16 * nch - q0, &s_win[t]};
         uint32_t need = uint32_t(min(L, uint64_t(16 * kWinChunks)));
         if (L >= 36 && 16 * nch >= q0 + 36) {
             const uint32_t mt = R1.be32(8);
@@ -509,16 +514,15 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
 #pragma unroll
             for (uint32_t j = kR2; j < kWinChunks; ++j) {
                 if (j >= nch && j < want) {
-                    s_win[(4 * j + 0) * kDecTile + t] = w[j - kR2].x;
-                    s_win[(4 * j + 1) * kDecTile + t] = w[j - kR2].y;
-                    s_win[(4 * j + 2) * kDecTile + t] = w[j - kR2].z;
-                    s_win[(4 * j + 3) * kDecTile + t] = w[j - kR2].w;
+                    const uint32_t e[4] = {w[j - kR2].x, w[j - kR2].y, w[j - kR2].z, w[j - kR2].w};
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; ++k) s_win[(4 * j + k - d0) * kDecTile + t] = e[k];   // j >= 3 > d0
                 }
             }
             nch = want;
         }
     }
-    const Rd R{base, q0, 16 * nch, &s_win[t]};
+    const Rd R{base, q0 & 3u, nch ? 16 * nch - q0 : 0u, &s_win[t]};
     onc_msg m;
     uint4* mz = reinterpret_cast<uint4*>(&m);
 #pragma unroll
