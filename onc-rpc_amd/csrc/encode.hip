@@ -291,6 +291,7 @@ struct ChunkPlan {
     uintptr_t A;
     int32_t slot;
     uint32_t sel;
+    uint32_t plen;           // full-interior spans: the record's streamed payload bytes (sel = o - its start)
 };
 
 template <bool kByte>
@@ -352,6 +353,35 @@ __device__ __forceinline__ ChunkPlan plan_chunk_interior(const ImgTile& T, uint3
     const uint32_t hi = min(max(int32_t(q.y - o), 0), 16) >> 2;
     P.sel = hasp ? ((1u << (hi - lo)) - 1u) << lo : 0u;
     return P;
+}
+
+// Word path, full-interior span (additionally every record of the span has
+// a streamed payload and the source of each of its chunks, header chunks
+// included, lies inside the arena): every chunk loads its own source bytes
+// unconditionally and each dword is payload iff its offset from the
+// record's payload start is below the payload length.
+__device__ __forceinline__ ChunkPlan plan_chunk_full(const ImgTile& T, uint32_t gsh, uint64_t B0, int32_t c) {
+    int r = T.map[c >> gsh];
+    if (gsh != 0)
+        while (c >= T.ent[r + 1].x) ++r;
+    const int4 m = T.ent[r];
+    const uint4 q = T.pay[r];
+    const int32_t s = c - (c >= m.z ? m.y : m.w);
+    ChunkPlan P;
+    P.slot = s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s);
+    const uint32_t o = uint32_t(c) << 4;
+    P.A = (uint64_t(q.z) | (uint64_t(q.w) << 32)) + B0 + o;
+    P.sel = o - q.x;
+    P.plen = q.y - q.x;
+    return P;
+}
+
+__device__ __forceinline__ void merge_words_full(const uint32_t X[4], const uint4& L, uint32_t d, uint32_t len,
+                                                 uint32_t v[4]) {
+    v[0] = d < len ? X[0] : L.x;
+    v[1] = d + 4u < len ? X[1] : L.y;
+    v[2] = d + 8u < len ? X[2] : L.z;
+    v[3] = d + 12u < len ? X[3] : L.w;
 }
 
 __device__ __forceinline__ void merge_words_inplace(const uint32_t X[4], const uint4& L, uint32_t sel, uint32_t v[4]) {
@@ -629,7 +659,7 @@ struct SpanHdr {
     uint32_t gsh;
     uint32_t byte_mode;
     uint32_t state;          // 0: nothing to stream, 1: stream, 2: no more spans
-    uint32_t interior;       // word path: every payload source window inside the arena (plan_chunk_interior)
+    uint32_t interior;       // word path: 1 every payload source window inside the arena (plan_chunk_interior), 2 every chunk source too (plan_chunk_full)
 };
 struct WsSlot {
     ImgTile T;
@@ -783,12 +813,17 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
     }
     // interior: the 16-byte-granular source windows of every payload of the
     // span (from its first to its last output chunk) lie inside the arena
-    bool inside = true;
+    bool inside = true, full = true;
     if (active && Splen >= 16) {
         const uint64_t head = Spst & 15u, tail = (16u - (Sen & 15u)) & 15u;
         inside = Spoff >= head && Spoff + Splen + tail <= a.bounds.payload_len;
+        // full: the record's own chunks from its first (cfa) on read inside the arena too
+        full = inside && Spoff >= Spst - (uint64_t(Scfa) << 4);
+    } else if (active && Slen != 0) {
+        full = false;                                  // a record without streamed payload: chunks need `hasp`
     }
     const bool interior = __all(inside);
+    const bool interior_full = __all(full);
     const uint64_t E = min(S1, a.out_cap);
     if (lane == 0) {
         W.T.ent[hi_rec - lo_rec] = make_int4(0x7FFFFFFF, 0, 0, 0);
@@ -800,7 +835,7 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
         h.gsh = gsh;
         h.byte_mode = S.byte_mode ? 1u : 0u;
         h.state = E > S0 ? 1u : 0u;
-        h.interior = interior && !S.byte_mode ? 1u : 0u;
+        h.interior = S.byte_mode || !interior ? 0u : (interior_full ? 2u : 1u);
         W.h = h;
     }
     S.lo_rec = hi_rec;
@@ -810,7 +845,7 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
 // steps of 64 * kU chunks, this wave taking steps part, part + nparts, ...
 // (same two-register-set pipeline); part 0 also writes the partial edge
 // chunks.
-template <int kU, int kNT, bool kByte, bool kInterior = false>
+template <int kU, int kNT, bool kByte, int kInterior = 0>
 __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile& T, const SpanHdr& h, int part,
                                                  int nparts, uintptr_t dummy) {
     const int lane = threadIdx.x & 63;
@@ -828,8 +863,9 @@ __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile
 #define ONC_ISSUE(P, X, L, base)                                                          \
     _Pragma("unroll") for (int u = 0; u < kU; ++u) {                                     \
         const int32_t c_ = min((base) + lane + 64 * u, cl - 1);                           \
-        P[u] = kInterior ? plan_chunk_interior(T, gsh, B0, c_, dummy)                     \
-                         : plan_chunk<kByte>(T, gsh, B0, c_, dummy);                      \
+        P[u] = kInterior == 2 ? plan_chunk_full(T, gsh, B0, c_)                           \
+             : kInterior == 1 ? plan_chunk_interior(T, gsh, B0, c_, dummy)                \
+                              : plan_chunk<kByte>(T, gsh, B0, c_, dummy);                 \
         load_chunk<kNT, kByte>(P[u], X[u]);                                               \
         L[u] = T.img[P[u].slot];                                                          \
     }
@@ -837,7 +873,8 @@ __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile
     _Pragma("unroll") for (int u = 0; u < kU; ++u) {                                     \
         const int32_t c = min((base) + lane + 64 * u, cl - 1);                            \
         uint32_t v[4];                                                                    \
-        if (kInterior) merge_words_inplace(X[u], L[u], P[u].sel, v);                      \
+        if (kInterior == 2) merge_words_full(X[u], L[u], P[u].sel, P[u].plen, v);         \
+        else if (kInterior == 1) merge_words_inplace(X[u], L[u], P[u].sel, v);            \
         else merge_chunk<kByte>(P[u], X[u], L[u], v);                                     \
         u32x4* d = reinterpret_cast<u32x4*>(a.out + B0 + (uint64_t(c) << 4));             \
         if (kNT & 2) __builtin_nontemporal_store(u32x4{v[0], v[1], v[2], v[3]}, d);        \
@@ -930,8 +967,10 @@ __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
         } else if (state == 1u) {
             const SpanHdr h = s_slot[cur].h;
             if (h.byte_mode) stream_span_part<1, kNT, true>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
+            else if (h.interior == 2 && !(a.variant & 0x8000))
+                stream_span_part<kU, kNT, false, 2>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
             else if (h.interior && !(a.variant & 0x4000))
-                stream_span_part<kU, kNT, false, true>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
+                stream_span_part<kU, kNT, false, 1>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
             else stream_span_part<kU, kNT, false>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
         }
 #ifdef ONC_EMIT_PROF
