@@ -205,7 +205,10 @@ typedef struct onc_unix_params {
  * Zero-length bodies and payloads are not checked (their offsets are never
  * dereferenced). The reference's owned types cannot express such a
  * reference; the check replaces an out-of-bounds read, not a reference
- * behaviour. */
+ * behaviour. The sizes must be true: the encoder may read any byte of
+ * [payload_arena, payload_arena + payload_len) (it loads whole 16-byte
+ * windows at each output chunk's own source bytes when they all lie in the
+ * arena), never a byte outside it. */
 typedef struct onc_batch {
     uint64_t               n;
     const onc_msg*         msgs;          /* [dev] n descriptors */
