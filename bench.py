@@ -457,7 +457,6 @@ ALG_PER_LAUNCH = {
     "iov_emit_kernel": lambda n, W, H: n * (64 + 32) + H + 96 * ALG_CTX["unix_refs"],
     "frame_chunks_kernel": lambda n, W, H: 0,
     "frame_write_kernel": lambda n, W, H: 8 * n,
-    "frame_coff_kernel": lambda n, W, H: 0,
     "frame_walk_kernel": lambda n, W, H: 0,
     "frame_counts_kernel": lambda n, W, H: 0,
     "frame_guess_kernel": lambda n, W, H: 0,

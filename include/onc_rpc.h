@@ -43,8 +43,11 @@ extern "C" {
 /* 2: onc_batch carries arena sizes (bounds-checked descriptors), onc_encode
  *    accepts any output address, retired kernel id ONC_K_ENC_FIXUP removed.
  * 3: timing id 10 is ONC_K_FRAME_OFFSETS (the framer's chunk verification
- *    now runs inside frame_chunks; ONC_K_FRAME_VERIFY is gone). */
-#define ONC_RPC_ABI_VERSION 3
+ *    now runs inside frame_chunks; ONC_K_FRAME_VERIFY is gone).
+ * 4: body-level roots (ONC_ROOT_*, onc_decode_body, onc_encode_body,
+ *    onc_encode_body_lengths); timing id 10 retired (ONC_K_FRAME_OFFSETS
+ *    gone, the framer ids after it move down by one). */
+#define ONC_RPC_ABI_VERSION 4
 
 /* ------------------------------------------------------------------------ */
 /* Wire discriminants (values are the on-wire u32s)                          */
@@ -95,6 +98,61 @@ extern "C" {
 /* Decode modes: the two reference decoders */
 #define ONC_DECODE_SLICE 0 /* TryFrom<&[u8]>  src/rpc_message.rs:235-271 */
 #define ONC_DECODE_BYTES 1 /* TryFrom<Bytes>  src/rpc_message.rs:273-314 */
+
+/* Roots: the reference type a body-level call decodes each record as, or
+ * serialises each descriptor as (onc_decode_body / onc_encode_body). The
+ * reference has TryFrom / serialise_into / serialised_len on every type of
+ * a message, not only on RpcMessage; each root is one of
+ * them. `param` is a per-record u32 the root needs (else ignored).
+ *                               decode (slice | Bytes)              encode (serialise_into)
+ *  RPC_MESSAGE      RpcMessage  rpc_message.rs:235-271 | :273-314   :136-164
+ *  MESSAGE_TYPE     MessageType from_cursor :39-45 | TryFrom :80-93 :55-68
+ *  CALL_BODY        CallBody    call_body.rs:168-175 | :177-210     :98-108
+ *  REPLY_BODY       ReplyBody   reply_body.rs:76-83 | :85-98        :45-56
+ *  ACCEPTED_REPLY   AcceptedReply accepted_reply.rs:79-86 | :88-105 :58-61
+ *  ACCEPTED_STATUS  AcceptedStatus :234-241 | :243-265              :195-211
+ *  REJECTED_REPLY   RejectedReply rejected_reply.rs:98-105 | :107-125 :61-73
+ *  AUTH_ERROR       AuthError   from_cursor :176-190 | TryFrom :215-236 :194-207
+ *  AUTH_FLAVOR      AuthFlavor  flavor.rs:177-184 | :186-222       :106-129
+ *  AUTH_UNIX_PARAMS AuthUnixParams from_cursor(r, expected_len = param)
+ *                               unix_params.rs:90-129 | TryFrom :248-276  :162-176
+ *  OPAQUE           Opaque (crate-private) from_wire(r, max_len = param)
+ *                               opaque.rs:72-98 | try_array bytes_ext.rs:25-42  :38-56
+ * Descriptor shape of a root's value (decode writes it, encode reads it;
+ * fields outside it are zero on decode and ignored on encode):
+ *  MESSAGE_TYPE     as RPC_MESSAGE without xid
+ *  CALL_BODY        msg_type CALL, u.call, cred, verf, payload
+ *  REPLY_BODY       msg_type REPLY, reply_stat, stat, auth_stat, u.mismatch,
+ *                   verf and payload (accepted)
+ *  ACCEPTED_REPLY   the same with reply_stat ACCEPTED
+ *  ACCEPTED_STATUS  msg_type REPLY, reply_stat ACCEPTED, stat, u.mismatch,
+ *                   payload (no verifier)
+ *  REJECTED_REPLY   msg_type REPLY, reply_stat DENIED, stat, u.mismatch / auth_stat
+ *  AUTH_ERROR       msg_type REPLY, reply_stat DENIED, stat AUTH_ERROR, auth_stat
+ *  AUTH_FLAVOR      msg_type CALL, the value in cred (AUTH_UNIX: decode slot 2i)
+ *  AUTH_UNIX_PARAMS msg_type CALL, cred kind UNIX (decode: slot 2i)
+ *  OPAQUE           msg_type CALL, cred kind NONE, its body = the opaque's
+ * A descriptor of another shape encodes as ONC_ENC_BAD_DESCRIPTOR. */
+#define ONC_ROOT_RPC_MESSAGE      0
+#define ONC_ROOT_MESSAGE_TYPE     1
+#define ONC_ROOT_CALL_BODY        2
+#define ONC_ROOT_REPLY_BODY       3
+#define ONC_ROOT_ACCEPTED_REPLY   4
+#define ONC_ROOT_ACCEPTED_STATUS  5
+#define ONC_ROOT_REJECTED_REPLY   6
+#define ONC_ROOT_AUTH_ERROR       7
+#define ONC_ROOT_AUTH_FLAVOR      8
+#define ONC_ROOT_AUTH_UNIX_PARAMS 9
+#define ONC_ROOT_OPAQUE           10
+#define ONC_ROOT_COUNT            11
+/* Largest opaque body the OPAQUE root encodes: the crate serialises Opaque
+ * only for auth bodies (<= 200, flavor.rs:110) and machine names (<= 255,
+ * unix_params.rs:149); a longer one is ONC_ENC_BAD_DESCRIPTOR. Decode takes
+ * max_len up to ONC_OPAQUE_MAX_LEN (the descriptor's 24-bit length field;
+ * the reference calls from_wire with 200 and 255 only): a larger param acts
+ * as ONC_OPAQUE_MAX_LEN. */
+#define ONC_OPAQUE_ENCODE_MAX 255u
+#define ONC_OPAQUE_MAX_LEN    0xFFFFFFu
 
 /* ------------------------------------------------------------------------ */
 /* Per-record status codes                                                   */
@@ -270,9 +328,8 @@ int onc_abi_version(void);
  * lenoff up to 8M records); ONC_K_FRAME_COUNTS the framer's count pass
  * (frame_cblk, or frame_counts ahead of the three-launch scan beyond 512k
  * chunks); ONC_K_FRAME_WRITE its start copy, which up to 512k chunks also
- * sums each chunk's first record index. ONC_K_FRAME_OFFSETS keeps its
- * number but no launch carries it any more (its offsets pass, frame_coff,
- * is folded into the start copy). */
+ * sums each chunk's first record index. The body-level calls use the ids of
+ * the kernels they launch (ONC_K_ENC_LEN / _ENC_EMIT / _DEC_PARSE). */
 #define ONC_K_ENC_LEN      0
 #define ONC_K_SCAN_TILES   1
 #define ONC_K_ENC_EMIT     2
@@ -283,11 +340,10 @@ int onc_abi_version(void);
 #define ONC_K_IOV_EMIT     7
 #define ONC_K_FRAME        8
 #define ONC_K_FRAME_WRITE  9
-#define ONC_K_FRAME_OFFSETS 10
-#define ONC_K_FRAME_WALK   11
-#define ONC_K_FRAME_COUNTS 12
-#define ONC_K_FRAME_GUESS  13
-#define ONC_K_COUNT        14
+#define ONC_K_FRAME_WALK   10
+#define ONC_K_FRAME_COUNTS 11
+#define ONC_K_FRAME_GUESS  12
+#define ONC_K_COUNT        13
 #define ONC_TIMING_ALL    (-1)
 int onc_codec_enable_timing(onc_codec* codec, int enable);
 int onc_codec_kernel_stats(onc_codec* codec, double* ms_total /*[ONC_K_COUNT]*/,
@@ -333,8 +389,12 @@ int onc_encode(onc_codec* codec, const onc_batch* batch,
  *   onc_encode_emit : the bytes, placed by that plan (enc_emit) — same
  *                     arguments and results as onc_encode.
  * The plan belongs to the handle: emit must name the batch last planned on
- * it (same msgs pointer and n, else ONC_RC_EINVAL), and the descriptors must
- * not change in between. onc_encode = plan + emit. */
+ * it (same msgs pointer and n) with the status array the plan filled (the
+ * plan's statuses stand, emit only adds ONC_ENC_WRITE_ZERO), else
+ * ONC_RC_EINVAL; any other call on the handle in between that uses its
+ * scratch (every encode, decode_lengths and scan_lengths call) discards the
+ * plan (then ONC_RC_EINVAL too). The descriptors must not change in between.
+ * onc_encode = plan + emit. */
 int onc_encode_plan(onc_codec* codec, const onc_batch* batch, int32_t* status, uint32_t* rec_len);
 int onc_encode_emit(onc_codec* codec, const onc_batch* batch, uint8_t* out, uint64_t out_cap,
                     uint64_t* rec_off, int32_t* status);
@@ -424,6 +484,43 @@ int onc_scan_lengths(onc_codec* codec, const uint32_t* rec_len, uint64_t n,
  * rule and errors as onc_decode. */
 int onc_decode_lengths(onc_codec* codec, const uint8_t* wire, const uint32_t* rec_len, uint64_t n,
                        uint64_t base, int mode, uint64_t* rec_off, const onc_decoded* out);
+
+/* ------------------------------------------------------------------------ */
+/* Body-level roots (ONC_ROOT_*)                                             */
+/* ------------------------------------------------------------------------ */
+
+/* Decode record i = wire[rec_off[i] .. rec_off[i+1]) as `root`'s TryFrom
+ * over exactly that slice (slice mode: a Cursor over it, so every opaque
+ * bound is the record; Bytes mode: a Bytes of it). Unlike RpcMessage, a body
+ * has no framing header and no trailing-bytes check (the reference's body
+ * TryFrom impls return what they parsed and ignore the rest).
+ *   param[dev, n]   : AUTH_UNIX_PARAMS slice mode: expected_len; OPAQUE:
+ *                     max_len (both modes); required for those, else ignored
+ *                     (may be NULL).
+ *   out             : as onc_decode (descriptor shape per root above).
+ *   consumed[dev, n]: optional: bytes the value occupies (the cursor's final
+ *                     position = its serialised_len(); Call / Success
+ *                     payloads extend to the record's end); 0 on error.
+ * ONC_ROOT_RPC_MESSAGE is onc_decode (consumed = the record length on OK).
+ * Same over-read rule as onc_decode. */
+int onc_decode_body(onc_codec* codec, int root, const uint8_t* wire, const uint64_t* rec_off, uint64_t n,
+                    int mode, const uint32_t* param, const onc_decoded* out, uint32_t* consumed);
+
+/* serialised_len() of every descriptor as `root` + the checks of that
+ * root's serialise_into: shape (ONC_ENC_BAD_DESCRIPTOR), construction panics
+ * (NAME_GT_255, GIDS_GT_16), a body >= 2^31 bytes (ONC_ENC_TOO_LONG: the
+ * RpcMessage limit, rpc_message.rs:146-151, applied to every root), and the
+ * assoc > 200 assert (flavor.rs:110) for roots that serialise an AuthFlavor
+ * (MESSAGE_TYPE, CALL_BODY, REPLY_BODY, ACCEPTED_REPLY, AUTH_FLAVOR).
+ * Outputs as onc_encode_lengths. */
+int onc_encode_body_lengths(onc_codec* codec, int root, const onc_batch* batch, uint32_t* rec_len,
+                            int32_t* status);
+
+/* Every descriptor serialised as `root` back to back into out — the batch
+ * form of `root`::serialise_into on one Cursor<Vec<u8>>. Same outputs, writer
+ * position and capacity rules as onc_encode. */
+int onc_encode_body(onc_codec* codec, int root, const onc_batch* batch, uint8_t* out, uint64_t out_cap,
+                    uint64_t* rec_off, int32_t* status, uint32_t* rec_len);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -128,11 +128,23 @@ public:
     using std::runtime_error::runtime_error;
 };
 
+enum class DecodeMode { Slice = ONC_DECODE_SLICE, Bytes = ONC_DECODE_BYTES };
+class Codec;
+
 // ----------------------------------------------------------------------------
 // AuthUnixParams — src/auth/unix_params.rs:72-245
 // ----------------------------------------------------------------------------
 class AuthUnixParams {
 public:
+    // AuthUnixParams::from_cursor(r, expected_len) over `buf` (slice rules,
+    // unix_params.rs:90-129) and TryFrom<Bytes> (:248-276); serialise_into
+    // (:162-176) / serialised_len (:219-230). Body-level decode/encode on the
+    // GPU (onc_decode_body / onc_encode_body, ONC_ROOT_AUTH_UNIX_PARAMS).
+    static AuthUnixParams from_cursor(Codec& codec, Bytes buf, uint32_t expected_len);
+    static AuthUnixParams try_from(Codec& codec, Bytes buf);
+    void serialise_into(Codec& codec, std::vector<uint8_t>& buf) const;
+    uint32_t serialised_len(Codec& codec) const;
+
     // AuthUnixParams::new (unix_params.rs:142-158): panics on a machine name
     // longer than 255 bytes (:149) or more than 16 gids (Gids, :47).
     AuthUnixParams(uint32_t stamp, Bytes machine_name, uint32_t uid, uint32_t gid, std::vector<uint32_t> gids)
@@ -195,6 +207,19 @@ public:
     }
 
     Kind kind() const { return kind_; }
+    // TryFrom<&[u8]> (flavor.rs:177-184) / TryFrom<Bytes> (:186-222);
+    // serialise_into (:106-129) / serialised_len (:154-174) — on the GPU.
+    static AuthFlavor try_from(Codec& codec, Bytes buf, DecodeMode mode = DecodeMode::Slice);
+    void serialise_into(Codec& codec, std::vector<uint8_t>& buf) const;
+    uint32_t serialised_len(Codec& codec) const;
+    // associated_data_len (flavor.rs:142-150; unix_params.rs:234-245): the
+    // body bytes without prefixes or padding (the value the 200-byte assert
+    // of serialise_into checks).
+    uint32_t associated_data_len() const {
+        if (kind_ == Kind::AuthUnix)
+            return uint32_t(12 + unix_->machine_name().len + 4 * unix_->gids_vec().size());
+        return data_ ? uint32_t(data_->len) : 0u;
+    }
     // Wire discriminant (flavor.rs:132-139).
     uint32_t id() const {
         switch (kind_) {
@@ -235,6 +260,11 @@ public:
         : program_(program), program_version_(program_version), procedure_(procedure),
           cred_(std::move(auth_credentials)), verf_(std::move(auth_verifier)), payload_(payload) {}
     uint32_t rpc_version() const { return 2; }   // RPC_VERSION call_body.rs:10
+    // TryFrom<&[u8]> (call_body.rs:168-175) / TryFrom<Bytes> (:177-210);
+    // serialise_into (:98-108) / serialised_len (:111-119) — on the GPU.
+    static CallBody try_from(Codec& codec, Bytes buf, DecodeMode mode = DecodeMode::Slice);
+    void serialise_into(Codec& codec, std::vector<uint8_t>& buf) const;
+    uint32_t serialised_len(Codec& codec) const;
     uint32_t program() const { return program_; }
     uint32_t program_version() const { return program_version_; }
     uint32_t procedure() const { return procedure_; }
@@ -283,6 +313,11 @@ public:
     Kind kind() const { return kind_; }
     std::pair<uint32_t, uint32_t> mismatch() const { return {low_, high_}; }
     AuthError auth_error() const { return err_; }
+    // TryFrom<&[u8]> (rejected_reply.rs:98-105) / TryFrom<Bytes> (:107-125);
+    // serialise_into (:61-73) / serialised_len (:76-95) — on the GPU.
+    static RejectedReply try_from(Codec& codec, Bytes buf, DecodeMode mode = DecodeMode::Slice);
+    void serialise_into(Codec& codec, std::vector<uint8_t>& buf) const;
+    uint32_t serialised_len(Codec& codec) const;
     bool operator==(const RejectedReply& o) const {
         return kind_ == o.kind_ && (kind_ == Kind::AuthError ? err_ == o.err_ : (low_ == o.low_ && high_ == o.high_));
     }
@@ -310,6 +345,11 @@ public:
     }
     static AcceptedStatus of(Kind k) { return AcceptedStatus(k); }
     Kind kind() const { return kind_; }
+    // TryFrom<&[u8]> (accepted_reply.rs:234-241) / TryFrom<Bytes> (:243-265);
+    // serialise_into (:195-211) / serialised_len (:214-231) — on the GPU.
+    static AcceptedStatus try_from(Codec& codec, Bytes buf, DecodeMode mode = DecodeMode::Slice);
+    void serialise_into(Codec& codec, std::vector<uint8_t>& buf) const;
+    uint32_t serialised_len(Codec& codec) const;
     Bytes payload() const { return payload_; }
     std::pair<uint32_t, uint32_t> mismatch() const { return {low_, high_}; }
     bool operator==(const AcceptedStatus& o) const {
@@ -332,6 +372,11 @@ public:
         : verf_(std::move(auth_verifier)), status_(std::move(status)) {}
     const AuthFlavor& auth_verifier() const { return verf_; }
     const AcceptedStatus& status() const { return status_; }
+    // TryFrom<&[u8]> (accepted_reply.rs:79-86) / TryFrom<Bytes> (:88-105);
+    // serialise_into (:58-61) / serialised_len (:64-66) — on the GPU.
+    static AcceptedReply try_from(Codec& codec, Bytes buf, DecodeMode mode = DecodeMode::Slice);
+    void serialise_into(Codec& codec, std::vector<uint8_t>& buf) const;
+    uint32_t serialised_len(Codec& codec) const;
     bool operator==(const AcceptedReply& o) const { return verf_ == o.verf_ && status_ == o.status_; }
 
 private:
@@ -347,6 +392,11 @@ public:
     const AcceptedReply* accepted() const { return std::get_if<AcceptedReply>(&v_); }
     const RejectedReply* denied() const { return std::get_if<RejectedReply>(&v_); }
     bool operator==(const ReplyBody& o) const { return v_ == o.v_; }
+    // TryFrom<&[u8]> (reply_body.rs:76-83) / TryFrom<Bytes> (:85-98);
+    // serialise_into (:45-56) / serialised_len (:60-73) — on the GPU.
+    static ReplyBody try_from(Codec& codec, Bytes buf, DecodeMode mode = DecodeMode::Slice);
+    void serialise_into(Codec& codec, std::vector<uint8_t>& buf) const;
+    uint32_t serialised_len(Codec& codec) const;
 
 private:
     explicit ReplyBody(AcceptedReply r) : v_(std::move(r)) {}
@@ -362,6 +412,11 @@ public:
     const CallBody* call_body() const { return std::get_if<CallBody>(&v_); }
     const ReplyBody* reply_body() const { return std::get_if<ReplyBody>(&v_); }
     bool operator==(const MessageType& o) const { return v_ == o.v_; }
+    // from_cursor (rpc_message.rs:39-45) / TryFrom<Bytes> (:80-93);
+    // serialise_into (:55-68) / serialised_len (:72-77) — on the GPU.
+    static MessageType try_from(Codec& codec, Bytes buf, DecodeMode mode = DecodeMode::Slice);
+    void serialise_into(Codec& codec, std::vector<uint8_t>& buf) const;
+    uint32_t serialised_len(Codec& codec) const;
 
 private:
     explicit MessageType(CallBody c) : v_(std::move(c)) {}
@@ -369,7 +424,10 @@ private:
     std::variant<CallBody, ReplyBody> v_;
 };
 
-enum class DecodeMode { Slice = ONC_DECODE_SLICE, Bytes = ONC_DECODE_BYTES };
+// AuthError::from_cursor (rejected_reply.rs:176-190) / TryFrom<Bytes>
+// (:215-236); serialise_into (:194-207) — on the GPU.
+AuthError auth_error_try_from(Codec& codec, Bytes buf, DecodeMode mode = DecodeMode::Slice);
+void serialise_into(Codec& codec, AuthError e, std::vector<uint8_t>& buf);
 
 // ----------------------------------------------------------------------------
 // Codec: one onc_codec handle (device + stream + scan scratch)
@@ -479,12 +537,25 @@ class BatchEncoder {
 public:
     // Describe one message (copies its borrowed bytes into the host arenas).
     void push(const RpcMessage& m);
+    // Body-level values (ONC_ROOT_*): a batch holds values of one type and
+    // is serialised as that type (onc_encode_body); mixing throws.
+    void push(const MessageType& m);
+    void push(const CallBody& c);
+    void push(const ReplyBody& r);
+    void push(const AcceptedReply& r);
+    void push(const AcceptedStatus& s);
+    void push(const RejectedReply& r);
+    void push(AuthError e);
+    void push(const AuthFlavor& a);
+    void push(const AuthUnixParams& p);
+    int root() const { return root_ < 0 ? ONC_ROOT_RPC_MESSAGE : root_; }
     size_t size() const { return msgs_.size(); }
     void clear() {
         msgs_.clear();
         unix_.clear();
         auth_.clear();
         payload_.clear();
+        root_ = -1;
     }
 
     // Encode every pushed message back to back and APPEND the bytes to `out`
@@ -500,6 +571,15 @@ public:
 private:
     void upload(onc_batch& b);
     void put_auth(const AuthFlavor& a, onc_auth& d);
+    void put_payload(Bytes p, onc_msg& d);
+    void put_call(const CallBody& c, onc_msg& d);
+    void put_accepted(const AcceptedReply& a, onc_msg& d);
+    void put_status(const AcceptedStatus& s, onc_msg& d);
+    void put_rejected(const RejectedReply& r, onc_msg& d);
+    void put_reply(const ReplyBody& r, onc_msg& d);
+    void set_root(int root);
+
+    int root_ = -1;
 
     std::vector<onc_msg> msgs_;
     std::vector<onc_unix_params> unix_;
@@ -591,49 +671,135 @@ inline void BatchEncoder::put_auth(const AuthFlavor& a, onc_auth& d) {
     }
 }
 
+inline void BatchEncoder::set_root(int root) {
+    if (root_ >= 0 && root_ != root) throw std::logic_error("BatchEncoder: values of different types in one batch");
+    root_ = root;
+}
+
+inline void BatchEncoder::put_payload(Bytes p, onc_msg& d) {
+    if (p.len > 0xFFFFFFFFull) throw std::runtime_error("message length exceeds maximum");
+    d.payload_len = uint32_t(p.len);
+    d.payload_off = payload_.size();
+    payload_.insert(payload_.end(), p.ptr, p.ptr + p.len);
+}
+
+inline void BatchEncoder::put_call(const CallBody& c, onc_msg& d) {
+    d.msg_type = ONC_MSG_CALL;
+    d.u.call.program = c.program();
+    d.u.call.program_version = c.program_version();
+    d.u.call.procedure = c.procedure();
+    put_auth(c.auth_credentials(), d.cred);
+    put_auth(c.auth_verifier(), d.verf);
+    put_payload(c.payload(), d);
+}
+
+inline void BatchEncoder::put_status(const AcceptedStatus& s, onc_msg& d) {
+    d.msg_type = ONC_MSG_REPLY;
+    d.reply_stat = ONC_REPLY_ACCEPTED;
+    d.stat = uint8_t(s.kind());
+    if (s.kind() == AcceptedStatus::Kind::Success) {
+        put_payload(s.payload(), d);
+    } else if (s.kind() == AcceptedStatus::Kind::ProgramMismatch) {
+        d.u.mismatch.low = s.mismatch().first;
+        d.u.mismatch.high = s.mismatch().second;
+    }
+}
+
+inline void BatchEncoder::put_accepted(const AcceptedReply& a, onc_msg& d) {
+    put_auth(a.auth_verifier(), d.verf);
+    put_status(a.status(), d);
+}
+
+inline void BatchEncoder::put_rejected(const RejectedReply& j, onc_msg& d) {
+    d.msg_type = ONC_MSG_REPLY;
+    d.reply_stat = ONC_REPLY_DENIED;
+    if (j.kind() == RejectedReply::Kind::RpcVersionMismatch) {
+        d.stat = ONC_REJECT_RPC_MISMATCH;
+        d.u.mismatch.low = j.mismatch().first;
+        d.u.mismatch.high = j.mismatch().second;
+    } else {
+        d.stat = ONC_REJECT_AUTH_ERROR;
+        d.auth_stat = uint8_t(j.auth_error());
+    }
+}
+
+inline void BatchEncoder::put_reply(const ReplyBody& r, onc_msg& d) {
+    if (const AcceptedReply* a = r.accepted()) put_accepted(*a, d);
+    else put_rejected(*r.denied(), d);
+}
+
 inline void BatchEncoder::push(const RpcMessage& m) {
+    set_root(ONC_ROOT_RPC_MESSAGE);
     onc_msg d{};
     d.xid = m.xid();
-    if (const CallBody* c = m.call_body()) {
-        d.msg_type = ONC_MSG_CALL;
-        d.u.call.program = c->program();
-        d.u.call.program_version = c->program_version();
-        d.u.call.procedure = c->procedure();
-        put_auth(c->auth_credentials(), d.cred);
-        put_auth(c->auth_verifier(), d.verf);
-        d.payload_len = uint32_t(c->payload().len);
-        d.payload_off = payload_.size();
-        if (c->payload().len > 0xFFFFFFFFull) throw std::runtime_error("message length exceeds maximum");
-        payload_.insert(payload_.end(), c->payload().ptr, c->payload().ptr + c->payload().len);
-    } else {
-        const ReplyBody* r = m.reply_body();
-        d.msg_type = ONC_MSG_REPLY;
-        if (const AcceptedReply* a = r->accepted()) {
-            d.reply_stat = ONC_REPLY_ACCEPTED;
-            put_auth(a->auth_verifier(), d.verf);
-            d.stat = uint8_t(a->status().kind());
-            if (a->status().kind() == AcceptedStatus::Kind::Success) {
-                d.payload_len = uint32_t(a->status().payload().len);
-                d.payload_off = payload_.size();
-                payload_.insert(payload_.end(), a->status().payload().ptr,
-                                a->status().payload().ptr + a->status().payload().len);
-            } else if (a->status().kind() == AcceptedStatus::Kind::ProgramMismatch) {
-                d.u.mismatch.low = a->status().mismatch().first;
-                d.u.mismatch.high = a->status().mismatch().second;
-            }
-        } else {
-            const RejectedReply* j = r->denied();
-            d.reply_stat = ONC_REPLY_DENIED;
-            if (j->kind() == RejectedReply::Kind::RpcVersionMismatch) {
-                d.stat = ONC_REJECT_RPC_MISMATCH;
-                d.u.mismatch.low = j->mismatch().first;
-                d.u.mismatch.high = j->mismatch().second;
-            } else {
-                d.stat = ONC_REJECT_AUTH_ERROR;
-                d.auth_stat = uint8_t(j->auth_error());
-            }
-        }
-    }
+    if (const CallBody* c = m.call_body()) put_call(*c, d);
+    else put_reply(*m.reply_body(), d);
+    msgs_.push_back(d);
+}
+
+inline void BatchEncoder::push(const MessageType& m) {
+    set_root(ONC_ROOT_MESSAGE_TYPE);
+    onc_msg d{};
+    if (const CallBody* c = m.call_body()) put_call(*c, d);
+    else put_reply(*m.reply_body(), d);
+    msgs_.push_back(d);
+}
+
+inline void BatchEncoder::push(const CallBody& c) {
+    set_root(ONC_ROOT_CALL_BODY);
+    onc_msg d{};
+    put_call(c, d);
+    msgs_.push_back(d);
+}
+
+inline void BatchEncoder::push(const ReplyBody& r) {
+    set_root(ONC_ROOT_REPLY_BODY);
+    onc_msg d{};
+    put_reply(r, d);
+    msgs_.push_back(d);
+}
+
+inline void BatchEncoder::push(const AcceptedReply& r) {
+    set_root(ONC_ROOT_ACCEPTED_REPLY);
+    onc_msg d{};
+    put_accepted(r, d);
+    msgs_.push_back(d);
+}
+
+inline void BatchEncoder::push(const AcceptedStatus& s) {
+    set_root(ONC_ROOT_ACCEPTED_STATUS);
+    onc_msg d{};
+    put_status(s, d);
+    msgs_.push_back(d);
+}
+
+inline void BatchEncoder::push(const RejectedReply& r) {
+    set_root(ONC_ROOT_REJECTED_REPLY);
+    onc_msg d{};
+    put_rejected(r, d);
+    msgs_.push_back(d);
+}
+
+inline void BatchEncoder::push(AuthError e) {
+    set_root(ONC_ROOT_AUTH_ERROR);
+    onc_msg d{};
+    put_rejected(RejectedReply::auth_error(e), d);
+    msgs_.push_back(d);
+}
+
+inline void BatchEncoder::push(const AuthFlavor& a) {
+    set_root(ONC_ROOT_AUTH_FLAVOR);
+    onc_msg d{};
+    d.msg_type = ONC_MSG_CALL;
+    put_auth(a, d.cred);
+    msgs_.push_back(d);
+}
+
+inline void BatchEncoder::push(const AuthUnixParams& p) {
+    set_root(ONC_ROOT_AUTH_UNIX_PARAMS);
+    onc_msg d{};
+    d.msg_type = ONC_MSG_CALL;
+    put_auth(AuthFlavor::unix(p), d.cred);
     msgs_.push_back(d);
 }
 
@@ -667,7 +833,7 @@ inline std::vector<uint32_t> BatchEncoder::serialised_lens(Codec& codec, std::ve
         upload(b);
         uint32_t* dl = static_cast<uint32_t*>(d_len_.ensure(n * 4));
         int32_t* ds = static_cast<int32_t*>(d_status_.ensure(n * 4));
-        codec.check(onc_encode_lengths(codec.get(), &b, dl, ds), "onc_encode_lengths");
+        codec.check(onc_encode_body_lengths(codec.get(), root(), &b, dl, ds), "onc_encode_body_lengths");
         codec.sync();
         detail::hip_check(hipMemcpy(lens.data(), dl, n * 4, hipMemcpyDeviceToHost), "D2H");
         detail::hip_check(hipMemcpy(st.data(), ds, n * 4, hipMemcpyDeviceToHost), "D2H");
@@ -691,7 +857,7 @@ inline std::vector<int32_t> BatchEncoder::serialise_into(Codec& codec, std::vect
         uint8_t* dout = static_cast<uint8_t*>(d_out_.ensure(total + 16));
         uint64_t* doff = static_cast<uint64_t*>(d_off_.ensure((n + 1) * 8));
         int32_t* ds = static_cast<int32_t*>(d_status_.ensure(n * 4));
-        codec.check(onc_encode(codec.get(), &b, dout, total, doff, ds, nullptr), "onc_encode");
+        codec.check(onc_encode_body(codec.get(), root(), &b, dout, total, doff, ds, nullptr), "onc_encode_body");
         codec.sync();
         const size_t base = out.size();
         out.resize(base + total);
@@ -843,5 +1009,143 @@ inline RpcMessage RpcMessage::try_from(Codec& codec, Bytes buf, DecodeMode mode)
     if (!r[0].ok()) throw r[0].error();
     return std::move(*r[0].message);
 }
+
+// ----------------------------------------------------------------------------
+// Body-level types (ONC_ROOT_*): TryFrom / serialise_into / serialised_len of
+// one type of the message tree, on the GPU (onc_decode_body /
+// onc_encode_body, batches of one like RpcMessage's single forms).
+// ----------------------------------------------------------------------------
+namespace detail {
+
+// One record decoded as `root`; throws the reference's Error on failure.
+struct BodyView {
+    onc_msg d{};
+    onc_unix_params unix[2]{};
+};
+
+inline BodyView decode_root(Codec& codec, int root, Bytes buf, DecodeMode mode, uint32_t param) {
+    DevBuf dw, doff, dp, dm, du, ds, d0, d1;
+    uint8_t* w = static_cast<uint8_t*>(dw.ensure(buf.len + 16));
+    if (buf.len) hip_check(hipMemcpy(w, buf.ptr, buf.len, hipMemcpyHostToDevice), "H2D");
+    const uint64_t off[2] = {0, buf.len};
+    uint64_t* o = static_cast<uint64_t*>(doff.ensure(sizeof(off)));
+    hip_check(hipMemcpy(o, off, sizeof(off), hipMemcpyHostToDevice), "H2D");
+    uint32_t* p = static_cast<uint32_t*>(dp.ensure(4));
+    hip_check(hipMemcpy(p, &param, 4, hipMemcpyHostToDevice), "H2D");
+    onc_decoded out{};
+    out.msgs = static_cast<onc_msg*>(dm.ensure(sizeof(onc_msg)));
+    out.unix_params = static_cast<onc_unix_params*>(du.ensure(2 * sizeof(onc_unix_params)));
+    out.status = static_cast<int32_t*>(ds.ensure(4));
+    out.aux0 = static_cast<uint32_t*>(d0.ensure(4));
+    out.aux1 = static_cast<uint32_t*>(d1.ensure(4));
+    codec.check(onc_decode_body(codec.get(), root, w, o, 1, int(mode), p, &out, nullptr), "onc_decode_body");
+    codec.sync();
+    BodyView v;
+    int32_t st = 0;
+    uint32_t a0 = 0, a1 = 0;
+    hip_check(hipMemcpy(&v.d, out.msgs, sizeof(onc_msg), hipMemcpyDeviceToHost), "D2H");
+    hip_check(hipMemcpy(v.unix, out.unix_params, sizeof(v.unix), hipMemcpyDeviceToHost), "D2H");
+    hip_check(hipMemcpy(&st, out.status, 4, hipMemcpyDeviceToHost), "D2H");
+    hip_check(hipMemcpy(&a0, out.aux0, 4, hipMemcpyDeviceToHost), "D2H");
+    hip_check(hipMemcpy(&a1, out.aux1, 4, hipMemcpyDeviceToHost), "D2H");
+    if (st != ONC_OK) throw Error(st, a0, a1);
+    return v;
+}
+
+inline AcceptedStatus status_view(const onc_msg& d, const uint8_t* wire) {
+    if (d.stat == ONC_ACCEPT_SUCCESS) return AcceptedStatus::success(Bytes(wire + d.payload_off, d.payload_len));
+    if (d.stat == ONC_ACCEPT_PROG_MISMATCH) return AcceptedStatus::program_mismatch(d.u.mismatch.low, d.u.mismatch.high);
+    return AcceptedStatus::of(AcceptedStatus::Kind(d.stat));
+}
+
+inline RejectedReply rejected_view(const onc_msg& d) {
+    return d.stat == ONC_REJECT_RPC_MISMATCH ? RejectedReply::rpc_version_mismatch(d.u.mismatch.low, d.u.mismatch.high)
+                                             : RejectedReply::auth_error(AuthError(d.auth_stat));
+}
+
+// serialised_len / serialise_into of one value pushed into a BatchEncoder.
+template <class T>
+inline uint32_t root_len(Codec& codec, const T& v) {
+    BatchEncoder e;
+    e.push(v);
+    std::vector<int32_t> st;
+    const uint32_t n = e.serialised_lens(codec, &st)[0];
+    RpcMessage::raise_encode_status(st[0]);
+    return n;
+}
+
+template <class T>
+inline void root_into(Codec& codec, const T& v, std::vector<uint8_t>& buf) {
+    BatchEncoder e;
+    e.push(v);
+    RpcMessage::raise_encode_status(e.serialise_into(codec, buf)[0]);
+}
+
+}  // namespace detail
+
+inline MessageType MessageType::try_from(Codec& codec, Bytes buf, DecodeMode mode) {
+    const detail::BodyView v = detail::decode_root(codec, ONC_ROOT_MESSAGE_TYPE, buf, mode, 0);
+    return detail::message_view(v.d, v.unix, buf.ptr).message();
+}
+inline void MessageType::serialise_into(Codec& codec, std::vector<uint8_t>& buf) const { detail::root_into(codec, *this, buf); }
+inline uint32_t MessageType::serialised_len(Codec& codec) const { return detail::root_len(codec, *this); }
+
+inline CallBody CallBody::try_from(Codec& codec, Bytes buf, DecodeMode mode) {
+    const detail::BodyView v = detail::decode_root(codec, ONC_ROOT_CALL_BODY, buf, mode, 0);
+    return *detail::message_view(v.d, v.unix, buf.ptr).call_body();
+}
+inline void CallBody::serialise_into(Codec& codec, std::vector<uint8_t>& buf) const { detail::root_into(codec, *this, buf); }
+inline uint32_t CallBody::serialised_len(Codec& codec) const { return detail::root_len(codec, *this); }
+
+inline ReplyBody ReplyBody::try_from(Codec& codec, Bytes buf, DecodeMode mode) {
+    const detail::BodyView v = detail::decode_root(codec, ONC_ROOT_REPLY_BODY, buf, mode, 0);
+    return *detail::message_view(v.d, v.unix, buf.ptr).reply_body();
+}
+inline void ReplyBody::serialise_into(Codec& codec, std::vector<uint8_t>& buf) const { detail::root_into(codec, *this, buf); }
+inline uint32_t ReplyBody::serialised_len(Codec& codec) const { return detail::root_len(codec, *this); }
+
+inline AcceptedReply AcceptedReply::try_from(Codec& codec, Bytes buf, DecodeMode mode) {
+    const detail::BodyView v = detail::decode_root(codec, ONC_ROOT_ACCEPTED_REPLY, buf, mode, 0);
+    return AcceptedReply(detail::auth_view(v.d.verf, v.unix, buf.ptr), detail::status_view(v.d, buf.ptr));
+}
+inline void AcceptedReply::serialise_into(Codec& codec, std::vector<uint8_t>& buf) const { detail::root_into(codec, *this, buf); }
+inline uint32_t AcceptedReply::serialised_len(Codec& codec) const { return detail::root_len(codec, *this); }
+
+inline AcceptedStatus AcceptedStatus::try_from(Codec& codec, Bytes buf, DecodeMode mode) {
+    const detail::BodyView v = detail::decode_root(codec, ONC_ROOT_ACCEPTED_STATUS, buf, mode, 0);
+    return detail::status_view(v.d, buf.ptr);
+}
+inline void AcceptedStatus::serialise_into(Codec& codec, std::vector<uint8_t>& buf) const { detail::root_into(codec, *this, buf); }
+inline uint32_t AcceptedStatus::serialised_len(Codec& codec) const { return detail::root_len(codec, *this); }
+
+inline RejectedReply RejectedReply::try_from(Codec& codec, Bytes buf, DecodeMode mode) {
+    return detail::rejected_view(detail::decode_root(codec, ONC_ROOT_REJECTED_REPLY, buf, mode, 0).d);
+}
+inline void RejectedReply::serialise_into(Codec& codec, std::vector<uint8_t>& buf) const { detail::root_into(codec, *this, buf); }
+inline uint32_t RejectedReply::serialised_len(Codec& codec) const { return detail::root_len(codec, *this); }
+
+inline AuthError auth_error_try_from(Codec& codec, Bytes buf, DecodeMode mode) {
+    return AuthError(detail::decode_root(codec, ONC_ROOT_AUTH_ERROR, buf, mode, 0).d.auth_stat);
+}
+inline void serialise_into(Codec& codec, AuthError e, std::vector<uint8_t>& buf) { detail::root_into(codec, e, buf); }
+
+inline AuthFlavor AuthFlavor::try_from(Codec& codec, Bytes buf, DecodeMode mode) {
+    const detail::BodyView v = detail::decode_root(codec, ONC_ROOT_AUTH_FLAVOR, buf, mode, 0);
+    return detail::auth_view(v.d.cred, v.unix, buf.ptr);
+}
+inline void AuthFlavor::serialise_into(Codec& codec, std::vector<uint8_t>& buf) const { detail::root_into(codec, *this, buf); }
+inline uint32_t AuthFlavor::serialised_len(Codec& codec) const { return detail::root_len(codec, *this); }
+
+inline AuthUnixParams AuthUnixParams::from_cursor(Codec& codec, Bytes buf, uint32_t expected_len) {
+    const detail::BodyView v =
+        detail::decode_root(codec, ONC_ROOT_AUTH_UNIX_PARAMS, buf, DecodeMode::Slice, expected_len);
+    return detail::auth_view(v.d.cred, v.unix, buf.ptr).unix_params();
+}
+inline AuthUnixParams AuthUnixParams::try_from(Codec& codec, Bytes buf) {
+    const detail::BodyView v = detail::decode_root(codec, ONC_ROOT_AUTH_UNIX_PARAMS, buf, DecodeMode::Bytes, 0);
+    return detail::auth_view(v.d.cred, v.unix, buf.ptr).unix_params();
+}
+inline void AuthUnixParams::serialise_into(Codec& codec, std::vector<uint8_t>& buf) const { detail::root_into(codec, *this, buf); }
+inline uint32_t AuthUnixParams::serialised_len(Codec& codec) const { return detail::root_len(codec, *this); }
 
 }  // namespace onc_rpc

@@ -25,9 +25,12 @@ struct onc_codec {
     uint64_t frame_chunk = onc::kFrameChunkDefault;   // ONC_RPC_FRAME_CHUNK at create (bytes, >= 64)
     bool force_scan = false;   // ONC_RPC_FORCE_SCAN=1 at create: always launch the block scan (tests)
     uint32_t variant = 0;      // ONC_RPC_VARIANT at create: kernel variant bits (A/B measurements)
-    // the batch whose plan (onc_encode_plan) the scratch holds
+    // the batch whose plan (onc_encode_plan) the scratch holds, and the
+    // status array that plan filled; every other call that writes the
+    // scratch discards it (forget_plan)
     const onc_msg* planned_msgs = nullptr;
     uint64_t planned_n = ~0ull;
+    const int32_t* planned_status = nullptr;
     uint32_t timing = 0;   // bitmask of ONC_K_* ids whose launches are bracketed
     struct Pending {
         int kernel;
@@ -88,6 +91,15 @@ int run(onc_codec* c, int kernel, const char* what, F&& launch) {
     return ONC_RC_OK;
 }
 
+// A call that writes the scratch words a plan lives in (tile / workgroup
+// totals) makes a pending onc_encode_plan unusable: onc_encode_emit refuses
+// it instead of placing records by another call's totals.
+void forget_plan(onc_codec* c) {
+    c->planned_n = ~0ull;
+    c->planned_msgs = nullptr;
+    c->planned_status = nullptr;
+}
+
 // scratch (u64 words): [tile_sum T | spare 2T | block_sum B | block_base B | 16]
 uint64_t scratch_words(uint64_t T) { return 3 * T + 2 * (T / 4 + 1) + 16; }
 
@@ -108,7 +120,7 @@ int ensure_scratch(onc_codec* c, uint64_t tiles) {
         return ONC_RC_ENOMEM;
     }
     c->scratch_tiles = want;
-    c->planned_n = ~0ull;       // a plan in the old scratch is gone
+    forget_plan(c);             // a plan in the old scratch is gone
     return ONC_RC_OK;
 }
 
@@ -233,7 +245,6 @@ const char* onc_kernel_name(int k) {
         case ONC_K_IOV_EMIT: return "iov_emit_kernel";
         case ONC_K_FRAME: return "frame_chunks_kernel";
         case ONC_K_FRAME_WRITE: return "frame_write_kernel";
-        case ONC_K_FRAME_OFFSETS: return "frame_coff_kernel";
         case ONC_K_FRAME_WALK: return "frame_walk_kernel";
         case ONC_K_FRAME_COUNTS: return "frame_counts_kernel";
         case ONC_K_FRAME_GUESS: return "frame_guess_kernel";
@@ -310,13 +321,15 @@ int onc_encode_lengths(onc_codec* c, const onc_batch* batch, uint32_t* rec_len, 
     a.status = status;
     a.rec_len = rec_len;
     bind_scratch(c, a);
+    forget_plan(c);
     return run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
 }
 
 namespace {
 
 // Encoder arguments common to the plan and emit phases.
-int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* rec_len, onc::EncArgs& a) {
+int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* rec_len, onc::EncArgs& a,
+             uint32_t root = ONC_ROOT_RPC_MESSAGE) {
     const uint64_t tiles = onc::num_emit_tiles(batch->n);
     const int rc = ensure_scratch(c, tiles);
     if (rc != ONC_RC_OK) return rc;
@@ -350,28 +363,35 @@ int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
     const bool big = batch->payload_len >= 512 * n;
     const bool ws_shape = batch->payload_len >= 128 * n && (onc::num_emit_tiles(n) <= kWsMaxTiles || big);
     a.ws = ((c->variant & 0x200) || (!(c->variant & 0x400) && n && ws_shape)) ? (big ? 2u : 1u) : 0u;
+    a.root = root;
+    if (root != ONC_ROOT_RPC_MESSAGE) a.ws = 0;   // body roots: the wave-per-tile kernel
     a.fused_base = (onc::num_len_blocks(n) <= onc::kFusedBlocks && !c->force_scan) || a.ws;
     return ONC_RC_OK;
 }
 
 // enc_len: plans + per-tile and per-workgroup byte totals into the scratch.
-int enc_plan(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* rec_len) {
+int enc_plan(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* rec_len,
+             uint32_t root = ONC_ROOT_RPC_MESSAGE) {
     onc::EncArgs a;
-    int rc = enc_args(c, batch, status, rec_len, a);
+    int rc = enc_args(c, batch, status, rec_len, a, root);
     if (rc != ONC_RC_OK) return rc;
+    forget_plan(c);
     rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
-    c->planned_msgs = batch->msgs;
-    c->planned_n = batch->n;
+    if (root == ONC_ROOT_RPC_MESSAGE) {
+        c->planned_msgs = batch->msgs;
+        c->planned_n = batch->n;
+        c->planned_status = status;
+    }
     return ONC_RC_OK;
 }
 
 // [scan of the workgroup totals, with the grand total into rec_off[n]] +
 // enc_emit: the bytes, placed by the plan in the scratch.
 int enc_emit(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
-             int32_t* status, uint32_t* rec_len) {
+             int32_t* status, uint32_t* rec_len, uint32_t root = ONC_ROOT_RPC_MESSAGE) {
     onc::EncArgs a;
-    int rc = enc_args(c, batch, status, rec_len, a);
+    int rc = enc_args(c, batch, status, rec_len, a, root);
     if (rc != ONC_RC_OK) return rc;
     // any writer position: the kernels work on 16-byte chunks from the
     // aligned address below `out`, whose first `origin` bytes are never written
@@ -413,6 +433,7 @@ int onc_encode_plan(onc_codec* c, const onc_batch* batch, int32_t* status, uint3
     if (batch->n == 0) {
         c->planned_msgs = batch->msgs;
         c->planned_n = 0;
+        c->planned_status = status;
         return ONC_RC_OK;
     }
     return enc_plan(c, batch, status, rec_len);
@@ -422,8 +443,9 @@ int onc_encode_emit(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t
                     int32_t* status) {
     if (!c || check_batch(batch) != ONC_RC_OK || !rec_off) return ONC_RC_EINVAL;
     if (batch->n && (!status || (!out && out_cap))) return ONC_RC_EINVAL;
-    // the plan in this handle's scratch must be of this batch
+    // the plan in this handle's scratch must be of this batch, with its statuses
     if (c->planned_n != batch->n || c->planned_msgs != batch->msgs) return ONC_RC_EINVAL;
+    if (batch->n && c->planned_status != status) return ONC_RC_EINVAL;
     if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
     if (batch->n == 0) {
         const hipError_t e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
@@ -448,6 +470,7 @@ int onc_encode_iov(onc_codec* c, const onc_batch* batch, uint8_t* hdr_out, uint6
     if (rc != ONC_RC_OK) return rc;
     const uint64_t T = c->scratch_tiles;
     const uint64_t B = T / 4 + 1;
+    forget_plan(c);
     onc::IovArgs a{};
     a.n = batch->n;
     a.msgs = batch->msgs;
@@ -597,6 +620,7 @@ int onc_decode_lengths(onc_codec* c, const uint8_t* wire, const uint32_t* rec_le
     int rc = ensure_scratch(c, std::max<uint64_t>(onc::num_tiles(n), wgs / 3 + 1));
     if (rc != ONC_RC_OK) return rc;
     const uint64_t T = c->scratch_tiles;
+    forget_plan(c);
     onc::DecArgs a{};
     a.n = n;
     a.wire = wire;
@@ -636,6 +660,7 @@ int onc_scan_lengths(onc_codec* c, const uint32_t* rec_len, uint64_t n, uint64_t
     if (rc != ONC_RC_OK) return rc;
     uint64_t* tile_sum = c->scratch;
     uint64_t* tile_base = c->scratch + c->scratch_tiles;
+    forget_plan(c);
     if (onc::scan_lengths_fused_ok(n) && !c->force_scan) {
         // two launches: 4096-record block totals, then every block sums the
         // totals before it and scans its own lengths
@@ -651,6 +676,56 @@ int onc_scan_lengths(onc_codec* c, const uint32_t* rec_len, uint64_t n, uint64_t
     if (rc != ONC_RC_OK) return rc;
     return run(c, ONC_K_LEN_APPLY, "len_apply",
                [&] { return onc::launch_len_apply(rec_len, n, tile_base, rec_off, c->stream); });
+}
+
+int onc_decode_body(onc_codec* c, int root, const uint8_t* wire, const uint64_t* rec_off, uint64_t n, int mode,
+                    const uint32_t* param, const onc_decoded* out, uint32_t* consumed) {
+    if (!c || !out || (mode != ONC_DECODE_SLICE && mode != ONC_DECODE_BYTES)) return ONC_RC_EINVAL;
+    if (root < 0 || root >= ONC_ROOT_COUNT) return ONC_RC_EINVAL;
+    if (n == 0) return ONC_RC_OK;
+    if (!rec_off || !out->msgs || !out->unix_params || !out->status || !out->aux0 || !out->aux1)
+        return ONC_RC_EINVAL;
+    // the roots whose reference decoder takes a length argument
+    if (!param && (root == ONC_ROOT_OPAQUE || (root == ONC_ROOT_AUTH_UNIX_PARAMS && mode == ONC_DECODE_SLICE)))
+        return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    onc::DecArgs a{};
+    a.n = n;
+    a.wire = wire;
+    a.rec_off = rec_off;
+    a.out = *out;
+    a.variant = c->variant;
+    a.root = uint32_t(root);
+    a.param = param;
+    a.consumed = consumed;
+    a.body = 1;
+    return run(c, ONC_K_DEC_PARSE, "decode", [&] { return onc::launch_decode(a, mode, c->stream); });
+}
+
+int onc_encode_body_lengths(onc_codec* c, int root, const onc_batch* batch, uint32_t* rec_len, int32_t* status) {
+    if (!c || root < 0 || root >= ONC_ROOT_COUNT || check_batch(batch) != ONC_RC_OK || (batch->n && (!rec_len || !status)))
+        return ONC_RC_EINVAL;
+    if (batch->n == 0) return ONC_RC_OK;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    onc::EncArgs a;
+    const int rc = enc_args(c, batch, status, rec_len, a, uint32_t(root));
+    if (rc != ONC_RC_OK) return rc;
+    forget_plan(c);
+    return run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
+}
+
+int onc_encode_body(onc_codec* c, int root, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
+                    int32_t* status, uint32_t* rec_len) {
+    if (!c || root < 0 || root >= ONC_ROOT_COUNT || check_batch(batch) != ONC_RC_OK || !rec_off) return ONC_RC_EINVAL;
+    if (batch->n && (!status || (!out && out_cap))) return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    if (batch->n == 0) {
+        const hipError_t e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
+        return e == hipSuccess ? ONC_RC_OK : fail(c, e, "hipMemsetAsync");
+    }
+    const int rc = enc_plan(c, batch, status, rec_len, uint32_t(root));
+    if (rc != ONC_RC_OK) return rc;
+    return enc_emit(c, batch, out, out_cap, rec_off, status, nullptr, uint32_t(root));
 }
 
 int32_t onc_expected_message_len(const uint8_t* data, uint64_t len, uint32_t* out) {

@@ -225,89 +225,11 @@ __device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_
     return r;
 }
 
-// ---------------------------------------------------------------------------
-// Encode word generator: stream word k of a planned record
-// ---------------------------------------------------------------------------
-
 struct EncSrc {
     const onc_unix_params* unix;
     uintptr_t auth_arena;
     uintptr_t payload_arena;
 };
-
-// Word j of an opaque_auth (flavor.rs:106-129): id, length, body words
-// (last one zero padded, opaque.rs:38-56) or the AUTH_UNIX params
-// (unix_params.rs:162-176).
-__device__ __forceinline__ uint32_t auth_word(const onc_auth& a, uint32_t j, const EncSrc& s) {
-    const uint32_t kind = a.kind_len >> 24;
-    if (j == 0) {
-        const uint32_t id = kind == ONC_KIND_UNKNOWN ? a.id : kind;
-        return bswap(id);
-    }
-    if (kind != ONC_KIND_UNIX) {
-        const uint32_t len = a.kind_len & 0xFFFFFFu;
-        if (j == 1) return bswap(len);
-        const uintptr_t b = s.auth_arena + a.ref;
-        return load4_masked(b + 4ull * (j - 2), b + len);
-    }
-    const onc_unix_params* u = s.unix + a.ref;
-    const uint32_t nl = u->name_len, nw = words4(nl), ng = u->ngids;
-    if (j == 1) return bswap(20u + 4u * nw + 4u * ng);    // AuthUnixParams::serialised_len
-    if (j == 2) return bswap(u->stamp);
-    if (j == 3) return bswap(nl);
-    j -= 4;
-    if (j < nw) {
-        const uintptr_t b = s.auth_arena + u->name_off;
-        return load4_masked(b + 4ull * j, b + nl);
-    }
-    j -= nw;
-    if (j == 0) return bswap(u->uid);
-    if (j == 1) return bswap(u->gid);
-    if (j == 2) return bswap(ng);
-    return bswap(u->gids[j - 3]);
-}
-
-// Header word k < hw of record (d, len, meta).
-__device__ __forceinline__ uint32_t header_word(const onc_msg& d, uint32_t len, uint32_t meta, uint32_t k,
-                                                const EncSrc& s) {
-    if (k == 0) return bswap((len - 4u) | 0x80000000u);   // rpc_message.rs:156
-    if (k == 1) return bswap(d.xid);
-    if (k == 2) return bswap(uint32_t(d.msg_type));
-    if (d.msg_type == ONC_MSG_CALL) {
-        if (k == 3) return bswap(2u);                      // RPC_VERSION call_body.rs:10
-        if (k == 4) return bswap(d.u.call.program);
-        if (k == 5) return bswap(d.u.call.program_version);
-        if (k == 6) return bswap(d.u.call.procedure);
-        k -= 7;
-        const uint32_t cw = meta_cw(meta);
-        if (k < cw) return auth_word(d.cred, k, s);
-        return auth_word(d.verf, k - cw, s);
-    }
-    if (k == 3) return bswap(uint32_t(d.reply_stat));
-    if (d.reply_stat == ONC_REPLY_ACCEPTED) {
-        k -= 4;
-        const uint32_t vw = meta_vw(meta);
-        if (k < vw) return auth_word(d.verf, k, s);
-        k -= vw;
-        if (k == 0) return bswap(uint32_t(d.stat));
-        if (k == 1) return bswap(d.u.mismatch.low);
-        return bswap(d.u.mismatch.high);
-    }
-    if (k == 4) return bswap(uint32_t(d.stat));
-    if (d.stat == ONC_REJECT_RPC_MISMATCH) return bswap(k == 5 ? d.u.mismatch.low : d.u.mismatch.high);
-    return bswap(uint32_t(d.auth_stat));
-}
-
-// Stream word k (any integer) of the record; zero outside [0, len).
-__device__ __forceinline__ uint32_t record_word(const onc_msg& d, uint32_t len, uint32_t meta, int64_t k,
-                                                const EncSrc& s) {
-    if (k < 0 || 4 * k >= int64_t(len)) return 0u;
-    const uint32_t hw = meta_hw(meta);
-    if (uint64_t(k) < hw) return header_word(d, len, meta, uint32_t(k), s);
-    const uint64_t j = uint64_t(k) - hw;
-    const uintptr_t b = s.payload_arena + d.payload_off;
-    return load4_masked(b + 4 * j, b + d.payload_len);
-}
 
 // Sequential serialiser of the header words of one planned record (the
 // serialise_into call chain in write order), used to stage headers in LDS.
@@ -334,17 +256,11 @@ struct ShiftSink {
     __device__ __forceinline__ void finish() { *dst = funnel(prev, 0u, sh); }
 };
 
-template <class Sink>
-__device__ __forceinline__ void put_auth_words(const onc_auth& a, const EncSrc& s, Sink& out) {
-    const uint32_t kind = a.kind_len >> 24;
-    out(bswap(kind == ONC_KIND_UNKNOWN ? a.id : kind));
-    if (kind != ONC_KIND_UNIX) {
-        const uint32_t len = a.kind_len & 0xFFFFFFu;
-        out(bswap(len));
-        const uintptr_t b = s.auth_arena + a.ref;
-        for (uint32_t j = 0; 4 * j < len; ++j) out(load4_masked(b + 4ull * j, b + len));
-        return;
-    }
+// AuthUnixParams::serialise_into (unix_params.rs:162-176) of unix-table
+// entry `ref`, preceded (kLen) by its serialised_len — the opaque length
+// AuthFlavor::serialise_into writes before it (flavor.rs:123-126).
+template <bool kLen, class Sink>
+__device__ __forceinline__ void put_unix_words(uint64_t ref, const EncSrc& s, Sink& out) {
     static_assert(sizeof(onc_unix_params) == 96 && offsetof(onc_unix_params, ngids) == 12 &&
                       offsetof(onc_unix_params, name_off) == 16 && offsetof(onc_unix_params, name_len) == 24 &&
                       offsetof(onc_unix_params, gids) == 32,
@@ -352,7 +268,7 @@ __device__ __forceinline__ void put_auth_words(const onc_auth& a, const EncSrc& 
     // the whole 96-byte parameter block in six dwordx4 loads issued together
     // (one memory round trip; field by field, each gid was a dependent load
     // between two sink writes)
-    const uintptr_t ua = reinterpret_cast<uintptr_t>(s.unix + a.ref);
+    const uintptr_t ua = reinterpret_cast<uintptr_t>(s.unix + ref);
     u32x4 q[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) q[k] = gload<u32x4>(ua + 16 * k);
@@ -361,7 +277,7 @@ __device__ __forceinline__ void put_auth_words(const onc_auth& a, const EncSrc& 
     const uint32_t nl = q[1].z;
     const uint32_t gids[ONC_MAX_GIDS] = {q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w,
                                          q[4].x, q[4].y, q[4].z, q[4].w, q[5].x, q[5].y, q[5].z, q[5].w};
-    out(bswap(20u + 4u * words4(nl) + 4u * ng));
+    if (kLen) out(bswap(20u + 4u * words4(nl) + 4u * ng));
     out(bswap(stamp));
     out(bswap(nl));
     const uintptr_t b = s.auth_arena + name_off;
@@ -374,30 +290,53 @@ __device__ __forceinline__ void put_auth_words(const onc_auth& a, const EncSrc& 
         if (j < ng) out(bswap(gids[j]));
 }
 
+// Opaque::serialise_into (opaque.rs:38-56) of an auth body: length, body
+// words, the last one zero padded.
 template <class Sink>
-__device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, Sink& out) {
-    out(bswap((len - 4u) | 0x80000000u));        // record mark, rpc_message.rs:156
-    out(bswap(d.xid));
-    out(bswap(uint32_t(d.msg_type)));
-    if (d.msg_type == ONC_MSG_CALL) {
-        out(bswap(2u));                           // RPC_VERSION call_body.rs:10
-        out(bswap(d.u.call.program));
-        out(bswap(d.u.call.program_version));
-        out(bswap(d.u.call.procedure));
-        put_auth_words(d.cred, s, out);
-        put_auth_words(d.verf, s, out);
+__device__ __forceinline__ void put_opaque_words(const onc_auth& a, const EncSrc& s, Sink& out) {
+    const uint32_t len = a.kind_len & 0xFFFFFFu;
+    out(bswap(len));
+    const uintptr_t b = s.auth_arena + a.ref;
+    for (uint32_t j = 0; 4 * j < len; ++j) out(load4_masked(b + 4ull * j, b + len));
+}
+
+// AuthFlavor::serialise_into (flavor.rs:106-129).
+template <class Sink>
+__device__ __forceinline__ void put_auth_words(const onc_auth& a, const EncSrc& s, Sink& out) {
+    const uint32_t kind = a.kind_len >> 24;
+    out(bswap(kind == ONC_KIND_UNKNOWN ? a.id : kind));
+    if (kind != ONC_KIND_UNIX) {
+        put_opaque_words(a, s, out);
         return;
     }
-    out(bswap(uint32_t(d.reply_stat)));
-    if (d.reply_stat == ONC_REPLY_ACCEPTED) {
-        put_auth_words(d.verf, s, out);
-        out(bswap(uint32_t(d.stat)));
-        if (d.stat == ONC_ACCEPT_PROG_MISMATCH) {
-            out(bswap(d.u.mismatch.low));
-            out(bswap(d.u.mismatch.high));
-        }
-        return;
+    put_unix_words<true>(a.ref, s, out);
+}
+
+// CallBody::serialise_into (call_body.rs:98-108) up to the raw payload.
+template <class Sink>
+__device__ __forceinline__ void put_call_words(const onc_msg& d, const EncSrc& s, Sink& out) {
+    out(bswap(2u));                           // RPC_VERSION call_body.rs:10
+    out(bswap(d.u.call.program));
+    out(bswap(d.u.call.program_version));
+    out(bswap(d.u.call.procedure));
+    put_auth_words(d.cred, s, out);
+    put_auth_words(d.verf, s, out);
+}
+
+// AcceptedStatus::serialise_into (accepted_reply.rs:195-211) up to a
+// Success payload.
+template <class Sink>
+__device__ __forceinline__ void put_accepted_status_words(const onc_msg& d, Sink& out) {
+    out(bswap(uint32_t(d.stat)));
+    if (d.stat == ONC_ACCEPT_PROG_MISMATCH) {
+        out(bswap(d.u.mismatch.low));
+        out(bswap(d.u.mismatch.high));
     }
+}
+
+// RejectedReply::serialise_into (rejected_reply.rs:61-73; AuthError :194-207).
+template <class Sink>
+__device__ __forceinline__ void put_rejected_words(const onc_msg& d, Sink& out) {
     out(bswap(uint32_t(d.stat)));
     if (d.stat == ONC_REJECT_RPC_MISMATCH) {
         out(bswap(d.u.mismatch.low));
@@ -407,9 +346,150 @@ __device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len,
     }
 }
 
+// ReplyBody::serialise_into (reply_body.rs:45-56; AcceptedReply
+// accepted_reply.rs:58-61) up to a Success payload.
+template <class Sink>
+__device__ __forceinline__ void put_reply_words(const onc_msg& d, const EncSrc& s, Sink& out) {
+    out(bswap(uint32_t(d.reply_stat)));
+    if (d.reply_stat == ONC_REPLY_ACCEPTED) {
+        put_auth_words(d.verf, s, out);
+        put_accepted_status_words(d, out);
+        return;
+    }
+    put_rejected_words(d, out);
+}
+
+// RpcMessage::serialise_into (rpc_message.rs:136-164; MessageType :55-68)
+// up to the raw payload.
+template <class Sink>
+__device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, Sink& out) {
+    out(bswap((len - 4u) | 0x80000000u));        // record mark, rpc_message.rs:156
+    out(bswap(d.xid));
+    out(bswap(uint32_t(d.msg_type)));
+    if (d.msg_type == ONC_MSG_CALL) put_call_words(d, s, out);
+    else put_reply_words(d, s, out);
+}
+
 __device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, uint32_t* dst) {
     WordSink w{dst};
     put_header_words(d, len, s, w);
+}
+
+// ---------------------------------------------------------------------------
+// Body-level roots (ONC_ROOT_*, include/onc_rpc.h): the serialised_len and
+// serialise_into of one type of the message tree instead of RpcMessage.
+// The header words of a root are a sub-sequence of the message's, written by
+// the same pieces above; a Call / Success payload still comes last.
+// ---------------------------------------------------------------------------
+
+// Does the descriptor have the shape of `root`'s value?
+__device__ __forceinline__ bool root_shape_ok(const onc_msg& d, uint32_t root) {
+    const bool call = d.msg_type == ONC_MSG_CALL, reply = d.msg_type == ONC_MSG_REPLY;
+    const bool acc = reply && d.reply_stat == ONC_REPLY_ACCEPTED, den = reply && d.reply_stat == ONC_REPLY_DENIED;
+    switch (root) {
+        case ONC_ROOT_MESSAGE_TYPE: return call || reply;
+        case ONC_ROOT_CALL_BODY:
+        case ONC_ROOT_AUTH_FLAVOR: return call;
+        case ONC_ROOT_AUTH_UNIX_PARAMS: return call && (d.cred.kind_len >> 24) == ONC_KIND_UNIX;
+        case ONC_ROOT_OPAQUE:
+            return call && (d.cred.kind_len >> 24) != ONC_KIND_UNIX && (d.cred.kind_len >> 24) <= ONC_KIND_UNKNOWN &&
+                   (d.cred.kind_len & 0xFFFFFFu) <= ONC_OPAQUE_ENCODE_MAX;
+        case ONC_ROOT_REPLY_BODY: return reply;
+        case ONC_ROOT_ACCEPTED_REPLY:
+        case ONC_ROOT_ACCEPTED_STATUS: return acc;
+        case ONC_ROOT_REJECTED_REPLY: return den;
+        case ONC_ROOT_AUTH_ERROR: return den && d.stat == ONC_REJECT_AUTH_ERROR;
+        default: return false;
+    }
+}
+
+// serialised_len of `root` + its serialise_into checks (see onc_encode_body_lengths):
+// shape, then the descriptor checks of plan_record for the parts the root
+// serialises, the 2^31 limit, and the assoc assert for roots that
+// serialise an AuthFlavor. meta: cw / vw as plan_record, hw = the root's
+// header words (everything before the payload).
+__device__ __forceinline__ RecPlan plan_root(const onc_msg& d, const onc_unix_params* unix, const Bounds& bd,
+                                             uint32_t root) {
+    if (root == ONC_ROOT_RPC_MESSAGE) return plan_record(d, unix, bd);
+    RecPlan r;
+    r.len = 0;
+    r.meta = 0;
+    r.status = ONC_OK;
+    if (!root_shape_ok(d, root)) { r.status = ONC_ENC_BAD_DESCRIPTOR; return r; }
+    uint32_t cw = 0, vw = 0, hw = 0;
+    uint64_t body = 0;
+    uint32_t assoc_c = 0, assoc_v = 0;
+    if (root == ONC_ROOT_AUTH_FLAVOR || root == ONC_ROOT_AUTH_UNIX_PARAMS || root == ONC_ROOT_OPAQUE) {
+        const AuthPlan c = plan_auth(d.cred, unix, bd);
+        if (c.status) { r.status = c.status; return r; }
+        cw = c.words;
+        // AuthFlavor: id + body; AuthUnixParams: without id and length;
+        // Opaque: without the id
+        hw = root == ONC_ROOT_AUTH_FLAVOR ? cw : (root == ONC_ROOT_AUTH_UNIX_PARAMS ? cw - 2 : cw - 1);
+        if (root == ONC_ROOT_AUTH_FLAVOR) assoc_c = c.assoc;
+    } else if (d.msg_type == ONC_MSG_CALL) {         // MESSAGE_TYPE, CALL_BODY
+        const AuthPlan c = plan_auth(d.cred, unix, bd);
+        if (c.status) { r.status = c.status; return r; }
+        const AuthPlan v = plan_auth(d.verf, unix, bd);
+        if (v.status) { r.status = v.status; return r; }
+        cw = c.words; vw = v.words;
+        assoc_c = c.assoc; assoc_v = v.assoc;
+        hw = (root == ONC_ROOT_MESSAGE_TYPE ? 1 : 0) + 4 + cw + vw;
+        body = d.payload_len;
+    } else if (d.reply_stat == ONC_REPLY_ACCEPTED) {  // MESSAGE_TYPE .. ACCEPTED_STATUS
+        if (d.stat > ONC_ACCEPT_SYSTEM_ERR) { r.status = ONC_ENC_BAD_DESCRIPTOR; return r; }
+        if (root != ONC_ROOT_ACCEPTED_STATUS) {
+            const AuthPlan v = plan_auth(d.verf, unix, bd);
+            if (v.status) { r.status = v.status; return r; }
+            vw = v.words; assoc_v = v.assoc;
+        }
+        hw = (root == ONC_ROOT_MESSAGE_TYPE ? 2 : (root == ONC_ROOT_REPLY_BODY ? 1 : 0)) + vw + 1 +
+             (d.stat == ONC_ACCEPT_PROG_MISMATCH ? 2 : 0);
+        body = d.stat == ONC_ACCEPT_SUCCESS ? d.payload_len : 0;
+    } else if (d.reply_stat == ONC_REPLY_DENIED) {    // MESSAGE_TYPE, REPLY_BODY, REJECTED_REPLY, AUTH_ERROR
+        if (d.stat > ONC_REJECT_AUTH_ERROR) { r.status = ONC_ENC_BAD_DESCRIPTOR; return r; }
+        if (d.stat == ONC_REJECT_AUTH_ERROR && d.auth_stat > ONC_AUTH_STAT_MAX) {
+            r.status = ONC_ENC_BAD_DESCRIPTOR; return r;
+        }
+        hw = root == ONC_ROOT_AUTH_ERROR ? 1
+                                         : (root == ONC_ROOT_MESSAGE_TYPE ? 2 : (root == ONC_ROOT_REPLY_BODY ? 1 : 0)) + 1 +
+                                               (d.stat == ONC_REJECT_RPC_MISMATCH ? 2 : 1);
+    } else {
+        r.status = ONC_ENC_BAD_DESCRIPTOR; return r;
+    }
+    if (body != 0 && !in_arena(d.payload_off, body, bd.payload_len)) { r.status = ONC_ENC_BAD_DESCRIPTOR; return r; }
+    const uint64_t total = 4ull * hw + body;
+    if (total & 0xFFFFFFFF80000000ull) { r.status = ONC_ENC_TOO_LONG; return r; }
+    if (assoc_c > ONC_MAX_AUTH_LEN || assoc_v > ONC_MAX_AUTH_LEN) { r.status = ONC_ENC_AUTH_GT_200; return r; }
+    r.len = total;
+    r.meta = cw | (vw << 8) | (hw << 16);
+    return r;
+}
+
+// The header words of `root` (a descriptor plan_root accepted), in write order.
+template <class Sink>
+__device__ __forceinline__ void put_root_words(const onc_msg& d, uint32_t len, const EncSrc& s, uint32_t root,
+                                               Sink& out) {
+    switch (root) {
+        case ONC_ROOT_RPC_MESSAGE: put_header_words(d, len, s, out); return;
+        case ONC_ROOT_MESSAGE_TYPE:
+            out(bswap(uint32_t(d.msg_type)));
+            if (d.msg_type == ONC_MSG_CALL) put_call_words(d, s, out);
+            else put_reply_words(d, s, out);
+            return;
+        case ONC_ROOT_CALL_BODY: put_call_words(d, s, out); return;
+        case ONC_ROOT_REPLY_BODY: put_reply_words(d, s, out); return;
+        case ONC_ROOT_ACCEPTED_REPLY:
+            put_auth_words(d.verf, s, out);
+            put_accepted_status_words(d, out);
+            return;
+        case ONC_ROOT_ACCEPTED_STATUS: put_accepted_status_words(d, out); return;
+        case ONC_ROOT_REJECTED_REPLY: put_rejected_words(d, out); return;
+        case ONC_ROOT_AUTH_ERROR: out(bswap(uint32_t(d.auth_stat))); return;
+        case ONC_ROOT_AUTH_FLAVOR: put_auth_words(d.cred, s, out); return;
+        case ONC_ROOT_AUTH_UNIX_PARAMS: put_unix_words<false>(d.cred.ref, s, out); return;
+        default: put_opaque_words(d.cred, s, out); return;    // ONC_ROOT_OPAQUE
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -393,6 +393,155 @@ __device__ __forceinline__ int32_t parse_record(const Rd& R, uint64_t L, uint64_
     }
     return ONC_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Body-level roots (onc_decode_body, ONC_ROOT_*): the TryFrom of one type of
+// the message tree over the whole record — no record-marking header, no
+// trailing-bytes check (the reference's body decoders return what they
+// parsed); `consumed` = the cursor's final position. Bound of every opaque:
+// the record (the Cursor / Bytes covers exactly the slice given).
+// ---------------------------------------------------------------------------
+
+// AuthUnixParams::from_cursor(r, expected_len) (unix_params.rs:90-129, slice)
+// / AuthUnixParams::try_from(Bytes) (:252-276: no consumed check).
+template <int MODE>
+__device__ __forceinline__ int32_t unix_params_root(const Rd& R, uint32_t& pos, uint32_t end, uint64_t rec_off,
+                                                    uint64_t slot, uint32_t expected, UnixSlots& us) {
+    constexpr int32_t kShort = Rules<MODE>::kShort;
+    const uint32_t start = pos;
+    uint32_t stamp, nl, uid, gid, ng;
+    ONC_RD(stamp);
+    ONC_RD(nl);                                                           // opaque.rs:76 / bytes_ext.rs:26
+    if (nl > ONC_MAX_MACHINE_NAME_LEN) return ONC_ERR_INVALID_LENGTH;
+    if (uint64_t(pos) + nl + pad4(nl) > end) return ONC_ERR_INVALID_LENGTH;
+    const uint32_t name_pos = pos;
+    pos += nl + pad4(nl);
+    ONC_RD(uid);
+    ONC_RD(gid);
+    ONC_RD(ng);
+    if (ng > ONC_MAX_GIDS) return ONC_ERR_INVALID_AUTH_DATA;             // unix_params.rs:112 / :266
+    if (uint64_t(pos) + 4ull * ng > end) return kShort;                  // every short gid read alike
+    uint32_t gids[ONC_MAX_GIDS];
+    R.words16(pos, ng, gids);
+    pos += 4u * ng;
+    if (MODE == ONC_DECODE_SLICE && pos - start != expected) return ONC_ERR_INVALID_AUTH_DATA;   // :117-119
+    put_unix(us, slot, stamp, uid, gid, ng, rec_off + name_pos, nl, gids);
+    return ONC_OK;
+}
+
+template <int MODE>
+__device__ __forceinline__ int32_t parse_root(const Rd& R, uint32_t end, uint64_t rec_off, uint64_t i, uint32_t root,
+                                              uint32_t param, onc_msg& m, uint32_t& aux0, UnixSlots& us,
+                                              uint32_t& consumed) {
+    constexpr int32_t kShort = Rules<MODE>::kShort;
+    uint32_t pos = 0, v;
+    if (root == ONC_ROOT_AUTH_FLAVOR || root == ONC_ROOT_AUTH_UNIX_PARAMS || root == ONC_ROOT_OPAQUE) {
+        m.msg_type = ONC_MSG_CALL;
+        int32_t st;
+        if (root == ONC_ROOT_AUTH_FLAVOR) {                    // flavor.rs:177-184 / :186-222
+            st = auth_any<MODE>(R, pos, end, rec_off, 2 * i, m.cred, us);
+        } else if (root == ONC_ROOT_AUTH_UNIX_PARAMS) {
+            st = unix_params_root<MODE>(R, pos, end, rec_off, 2 * i, param, us);
+            m.cred.id = ONC_AUTH_UNIX;
+            m.cred.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
+            m.cred.ref = 2 * i;
+        } else {                                               // opaque.rs:72-98 / bytes_ext.rs:25-42
+            const uint32_t max_len = min(param, ONC_OPAQUE_MAX_LEN);
+            uint32_t n;
+            ONC_RD(n);
+            if (n > max_len) return ONC_ERR_INVALID_LENGTH;
+            if (uint64_t(pos) + n + pad4(n) > end) return ONC_ERR_INVALID_LENGTH;
+            m.cred.kind_len = ONC_AUTH_PACK(ONC_KIND_NONE, n);
+            m.cred.ref = rec_off + pos;
+            pos += n + pad4(n);
+            st = ONC_OK;
+        }
+        consumed = pos;
+        return st;
+    }
+    uint32_t node = root;
+    if (node == ONC_ROOT_MESSAGE_TYPE) {                       // rpc_message.rs:39-45 / :84-92
+        ONC_RD(v);
+        if (v == ONC_MSG_CALL) node = ONC_ROOT_CALL_BODY;
+        else if (v == ONC_MSG_REPLY) node = ONC_ROOT_REPLY_BODY;
+        else { aux0 = v; return ONC_ERR_INVALID_MESSAGE_TYPE; }
+    }
+    if (node == ONC_ROOT_CALL_BODY) {                          // call_body.rs:37-69 / :181-209
+        m.msg_type = ONC_MSG_CALL;
+        uint32_t rv;
+        ONC_RD(rv);
+        if (rv != 2u) { aux0 = rv; return ONC_ERR_INVALID_RPC_VERSION; }
+        ONC_RD(m.u.call.program);
+        ONC_RD(m.u.call.program_version);
+        ONC_RD(m.u.call.procedure);
+        int32_t st = auth_any<MODE>(R, pos, end, rec_off, 2 * i, m.cred, us);
+        if (st != ONC_OK) return st;
+        st = auth_any<MODE>(R, pos, end, rec_off, 2 * i + 1, m.verf, us);
+        if (st != ONC_OK) return st;
+        m.payload_off = rec_off + pos;
+        m.payload_len = end - pos;
+        consumed = end;
+        return ONC_OK;
+    }
+    m.msg_type = ONC_MSG_REPLY;
+    if (node == ONC_ROOT_REPLY_BODY) {                         // reply_body.rs:29-35 / :89-97
+        ONC_RD(v);
+        if (v == ONC_REPLY_ACCEPTED) node = ONC_ROOT_ACCEPTED_REPLY;
+        else if (v == ONC_REPLY_DENIED) node = ONC_ROOT_REJECTED_REPLY;
+        else { aux0 = v; return ONC_ERR_INVALID_REPLY_TYPE; }
+    }
+    if (node == ONC_ROOT_ACCEPTED_REPLY) {                     // accepted_reply.rs:35-40 / :92-104
+        m.reply_stat = ONC_REPLY_ACCEPTED;
+        const int32_t st = auth_any<MODE>(R, pos, end, rec_off, 2 * i + 1, m.verf, us);
+        if (st != ONC_OK) return st;
+        node = ONC_ROOT_ACCEPTED_STATUS;
+    }
+    if (node == ONC_ROOT_ACCEPTED_STATUS) {                    // accepted_reply.rs:158-186 / :247-264
+        m.reply_stat = ONC_REPLY_ACCEPTED;
+        ONC_RD(v);
+        m.stat = uint8_t(v);
+        switch (v) {
+            case ONC_ACCEPT_SUCCESS:
+                m.payload_off = rec_off + pos;
+                m.payload_len = end - pos;
+                pos = end;
+                break;
+            case ONC_ACCEPT_PROG_UNAVAIL:
+            case ONC_ACCEPT_PROC_UNAVAIL:
+            case ONC_ACCEPT_GARBAGE_ARGS:
+            case ONC_ACCEPT_SYSTEM_ERR:
+                break;
+            case ONC_ACCEPT_PROG_MISMATCH:
+                ONC_RD(m.u.mismatch.low);
+                ONC_RD(m.u.mismatch.high);
+                break;
+            default:
+                aux0 = v;
+                return ONC_ERR_INVALID_REPLY_STATUS;
+        }
+        consumed = pos;
+        return ONC_OK;
+    }
+    m.reply_stat = ONC_REPLY_DENIED;
+    if (node == ONC_ROOT_REJECTED_REPLY) {                     // rejected_reply.rs:46-57 / :111-124
+        ONC_RD(v);
+        m.stat = uint8_t(v);
+        if (v == ONC_REJECT_RPC_MISMATCH) {
+            ONC_RD(m.u.mismatch.low);
+            ONC_RD(m.u.mismatch.high);
+            consumed = pos;
+            return ONC_OK;
+        }
+        if (v != ONC_REJECT_AUTH_ERROR) { aux0 = v; return ONC_ERR_INVALID_REJECTED_REPLY_TYPE; }
+    }
+    // AuthError (rejected_reply.rs:176-190 / :219-235)
+    m.stat = ONC_REJECT_AUTH_ERROR;
+    ONC_RD(v);
+    if (v > ONC_AUTH_STAT_MAX) { aux0 = v; return ONC_ERR_INVALID_AUTH_ERROR; }
+    m.auth_stat = uint8_t(v);
+    consumed = pos;
+    return ONC_OK;
+}
 #undef ONC_RD
 
 // decode_kernel: lane per record. The 64-byte descriptors of the
@@ -415,7 +564,11 @@ __device__ __forceinline__ int32_t parse_record(const Rd& R, uint64_t L, uint64_
 // the whole batch (onc_scan_lengths: 8 bytes written and read back per
 // record, one launch more).
 static_assert(kDecTile == 64, "kFromLen: one wave per workgroup, 64 workgroup totals per block");
-template <int MODE, bool kExact = false, bool kNTOut = false, bool kFromLen = false, bool kBlkFused = false>
+// kRoot (onc_decode_body): a.root selects the decoded type; the window
+// takes the record's first kWinChunks chunks in two rounds (the header-extent
+// guess below is the RpcMessage layout's).
+template <int MODE, bool kExact = false, bool kNTOut = false, bool kFromLen = false, bool kBlkFused = false,
+          bool kRoot = false>
 __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     __shared__ uint32_t s_win[kWinWords * kDecTile];
     static_assert(kWinWords * kDecTile * 4 >= kDecTile * sizeof(onc_msg), "descriptor staging reuses the window");
@@ -462,7 +615,7 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     uint32_t nch = 0;
     if (L != 0) {
         const uint32_t avail = uint32_t(min(uint64_t(kWinChunks), (q0 + L + 15) >> 4));
-        const uint32_t r1 = kExact ? uint32_t(min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4)) : kWin1;
+        const uint32_t r1 = kExact && !kRoot ? uint32_t(min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4)) : kWin1;
         nch = min(r1, avail);
         u32x4 v[kWin1];
 #pragma unroll
@@ -484,7 +637,7 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
         // accepted verifier.
         const Rd R1{base, q0 & 3u, 16 * nch - q0, &s_win[t]};
         uint32_t need = uint32_t(min(L, uint64_t(16 * kWinChunks)));
-        if (L >= 36 && 16 * nch >= q0 + 36) {
+        if (!kRoot && L >= 36 && 16 * nch >= q0 + 36) {
             const uint32_t mt = R1.be32(8);
             if (mt == ONC_MSG_CALL) {
                 const uint32_t cl = R1.be32(32);
@@ -506,7 +659,7 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
         if (want > nch) {
             // chunks [nch, want): from kR2 on (the first chunk round 1 may
             // have skipped) up to the window's end
-            constexpr uint32_t kR2 = kExact ? 3u : kWin1;   // round 1 held >= 3 chunks if L >= 44
+            constexpr uint32_t kR2 = kExact && !kRoot ? 3u : kWin1;   // round 1 held >= 3 chunks if L >= 44
             u32x4 w[kWinChunks > kR2 ? kWinChunks - kR2 : 1];
 #pragma unroll
             for (uint32_t j = kR2; j < kWinChunks; ++j)
@@ -534,12 +687,27 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
 #ifdef ONC_DEC_LEAN
     us.out = a.out.unix_params;
 #endif
+    uint32_t consumed = 0;
     if (valid) {
-        st = parse_record<MODE>(R, L, b, i, m, aux0, aux1, us);
+        if constexpr (kRoot) {
+            // records of 4 GiB or more: their payload does not fit the
+            // descriptor's 32-bit length
+            if (a.root == ONC_ROOT_RPC_MESSAGE) {
+                st = parse_record<MODE>(R, L, b, i, m, aux0, aux1, us);
+                consumed = uint32_t(L);               // an RpcMessage is the whole record
+            } else {
+                st = L > 0xFFFFFFFFull ? ONC_ERR_INVALID_LENGTH
+                                       : parse_root<MODE>(R, uint32_t(L), b, i, a.root, a.param ? a.param[i] : 0u, m,
+                                                          aux0, us, consumed);
+            }
+        } else {
+            st = parse_record<MODE>(R, L, b, i, m, aux0, aux1, us);
+        }
         if (st != ONC_OK) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);
         }
+        if (kRoot && a.consumed) a.consumed[i] = st == ONC_OK ? consumed : 0u;
         if (kNTOut) {
             __builtin_nontemporal_store(st, a.out.status + i);
             __builtin_nontemporal_store(aux0, a.out.aux0 + i);
@@ -658,6 +826,16 @@ hipError_t launch_dlen_tiles(const uint32_t* rec_len, uint64_t n, uint64_t* tile
 }
 
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s) {
+    if (a.body) {
+        const uint64_t tiles = (a.n + kDecTile - 1) / kDecTile;
+        if (mode == ONC_DECODE_BYTES)
+            ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true, false, false, true>), dim3(uint32_t(tiles)),
+                       dim3(kDecTile), 0, s, a);
+        else
+            ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true, false, false, true>), dim3(uint32_t(tiles)),
+                       dim3(kDecTile), 0, s, a);
+        return hipGetLastError();
+    }
     if (a.rec_len) {
         const uint64_t wgs = (a.n + kDecTile - 1) / kDecTile;
         const bool fused = a.blk_base == nullptr;

@@ -33,6 +33,10 @@ namespace onc {
 // rounds of workgroups.
 constexpr int kLenPer = 2;
 constexpr int kLenThreads = kLenRecs / kLenPer;
+// kRoot: a.root selects the serialised type (onc_encode_body, ONC_ROOT_*);
+// otherwise RpcMessage (the product encode, instantiated without the root
+// switch).
+template <bool kRoot>
 __global__ __launch_bounds__(kLenThreads) void enc_len_kernel(EncArgs a) {
     __shared__ uint64_t s_wave[kLenThreads / 64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -49,7 +53,7 @@ __global__ __launch_bounds__(kLenThreads) void enc_len_kernel(EncArgs a) {
         const uint64_t r = rw + 64 * k + lane;
         uint64_t len = 0;
         if (r < a.n) {
-            const RecPlan p = plan_record(d[k], a.unix, a.bounds);
+            const RecPlan p = kRoot ? plan_root(d[k], a.unix, a.bounds, a.root) : plan_record(d[k], a.unix, a.bounds);
             len = p.len;
             a.status[r] = p.status;
             if (a.rec_len) a.rec_len[r] = uint32_t(len);
@@ -500,7 +504,7 @@ __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, 
     }
 }
 
-template <int kU, int kNT, bool kFused, int kPipe = 2>
+template <int kU, int kNT, bool kFused, int kPipe = 2, bool kRoot = false>
 __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = tile * kEmitRecs;
@@ -532,7 +536,8 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     bool word_aligned = true;
     if (lane < nrec) {
         const onc_msg& d = dm;
-        const RecPlan p = plan_record(d, a.unix, a.bounds);   // the same function as enc_len: lengths agree
+        // the same function as enc_len: lengths agree
+        const RecPlan p = kRoot ? plan_root(d, a.unix, a.bounds, a.root) : plan_record(d, a.unix, a.bounds);
         len = p.len;
         hw = len ? meta_hw(p.meta) : 0;
         poff = d.payload_off;
@@ -609,12 +614,24 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                 const onc_msg d = as_msg(mr2);
                 const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
                 ImgSink w{img32, uint32_t(ibb >> 2), 32u - 8u * uint32_t(ibb & 3), 0u};
-                put_header_words(d, uint32_t(len), src, w);
+                if (kRoot) put_root_words(d, uint32_t(len), src, a.root, w);
+                else put_header_words(d, uint32_t(len), src, w);
                 if (small) {
                     // all of it lies in non-pure chunks (np = 0): right after
                     // the header (bytes past its end read as zero)
                     const uintptr_t pb = sb + pst;
                     for (uint32_t k = 0; 4 * k < plen; ++k) w(load4_masked(pb + 4 * k, pb + plen));
+                } else if (kRoot && pst < (uint64_t(cfa) << 4)) {
+                    // a body root's header can be shorter than a chunk
+                    // (AcceptedStatus: 4 bytes): payload bytes in the chunk
+                    // the record starts in belong to a chunk the record
+                    // before owns, whose stream loads only its own payload —
+                    // they go into the image (the rest streams from chunk
+                    // cfa on). A message header (>= 24 bytes) always ends
+                    // past that chunk.
+                    const uintptr_t pb = sb + pst;
+                    const uint32_t h = uint32_t((uint64_t(cfa) << 4) - pst);
+                    for (uint32_t k = 0; 4 * k < h; ++k) w(load4_masked(pb + 4 * k, pb + h));
                 }
                 w.finish();
                 // granules whose first chunk this record owns (chunk 0 of a
@@ -1005,15 +1022,19 @@ __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
 #ifndef ONC_EMIT_OCC
 #define ONC_EMIT_OCC 0   // lab: waves per SIMD the wave-per-tile kernel's registers must allow (0 = free: 106 VGPRs, 4)
 #endif
-template <int kU, int kNT = 0, int kOcc = 0, bool kFused = false, int kPipe = 2>
+template <int kU, int kNT = 0, int kOcc = 0, bool kFused = false, int kPipe = 2, bool kRoot = false>
 __global__ __launch_bounds__(64 * kFastWaves, kOcc ? kOcc * kFastWaves / 4 : 1) void enc_emit_kernel_t(EncArgs a) {
     __shared__ ImgTile s_tiles[kFastWaves];
     const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
-    if (tile < num_emit_tiles(a.n)) enc_emit_tile<kU, kNT, kFused, kPipe>(a, s_tiles[threadIdx.x >> 6], tile);
+    if (tile < num_emit_tiles(a.n))
+        enc_emit_tile<kU, kNT, kFused, kPipe, kRoot>(a, s_tiles[threadIdx.x >> 6], tile);
 }
 
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
-    ONC_LAUNCH(enc_len_kernel, dim3(uint32_t(num_len_blocks(a.n))), dim3(kLenThreads), 0, s, a);
+    if (a.root != ONC_ROOT_RPC_MESSAGE)
+        ONC_LAUNCH(enc_len_kernel<true>, dim3(uint32_t(num_len_blocks(a.n))), dim3(kLenThreads), 0, s, a);
+    else
+        ONC_LAUNCH(enc_len_kernel<false>, dim3(uint32_t(num_len_blocks(a.n))), dim3(kLenThreads), 0, s, a);
     return hipGetLastError();
 }
 
@@ -1027,6 +1048,17 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     const uint64_t blocks = (num_emit_tiles(a.n) + kFastWaves - 1) / kFastWaves;
+    if (a.root != ONC_ROOT_RPC_MESSAGE) {
+        // body-level roots (onc_encode_body): the wave-per-tile kernel with
+        // the root switch (codec.hip never picks the wave-specialised one)
+        if (a.fused_base)
+            ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, true, 2, true>), dim3(uint32_t(blocks)),
+                       dim3(64 * kFastWaves), 0, s, a);
+        else
+            ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, false, 2, true>), dim3(uint32_t(blocks)),
+                       dim3(64 * kFastWaves), 0, s, a);
+        return hipGetLastError();
+    }
     if (a.fused_base)
         ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, ONC_EMIT_OCC, true>), dim3(uint32_t(blocks)),
                            dim3(64 * kFastWaves), 0, s, a);

@@ -51,8 +51,9 @@ struct EncArgs {
     uint64_t* block_sum;    // enc_len workgroups (kLenRecs records): byte totals
     uint64_t* block_base;   // exclusive scan of block_sum (unused when fused_base)
     uint32_t fused_base;    // enc_emit sums block_sum itself (<= kFusedBlocks workgroups; no scan launch)
-    uint32_t variant;
-    uint32_t ws;            // enc_emit: the wave-specialised kernel (codec.hip enc_args decides)       // ONC_RPC_VARIANT bits (A/B experiments)
+    uint32_t variant;       // ONC_RPC_VARIANT bits (A/B experiments)
+    uint32_t ws;            // enc_emit: the wave-specialised kernel (codec.hip enc_args decides)
+    uint32_t root;          // ONC_ROOT_* (onc_encode_body); ONC_ROOT_RPC_MESSAGE for onc_encode
 #ifdef ONC_EMIT_PROF
     uint64_t* prof;         // lab builds only (tools/emit_prof.hip): per-tile phase timestamps
 #endif
@@ -125,6 +126,11 @@ struct DecArgs {
     uint64_t nblk;
     uint64_t base;              // offset of record 0
     uint64_t* rec_off_out;      // optional: the offsets (n + 1)
+    // onc_decode_body
+    uint32_t body;              // 1: the root kernel (decode_kernel<..., kRoot>)
+    uint32_t root;              // ONC_ROOT_*; ONC_ROOT_RPC_MESSAGE = the product decode
+    const uint32_t* param;      // per record: expected_len / max_len (or NULL)
+    uint32_t* consumed;         // optional: bytes the decoded value occupies
 };
 constexpr uint64_t kDecLenBlk = 4096;          // records per length block
 constexpr uint64_t kDecLenFusedBlocks = 512;   // up to 2M records: block totals summed in the decode

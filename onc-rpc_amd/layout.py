@@ -28,6 +28,14 @@ MSG_CALL, MSG_REPLY = 0, 1
 REPLY_ACCEPTED, REPLY_DENIED = 0, 1
 KIND_NONE, KIND_UNIX, KIND_SHORT, KIND_UNKNOWN = 0, 1, 2, 3
 DECODE_SLICE, DECODE_BYTES = 0, 1
+# body-level roots (include/onc_rpc.h ONC_ROOT_*): the reference type a
+# record is decoded / serialised as
+(ROOT_RPC_MESSAGE, ROOT_MESSAGE_TYPE, ROOT_CALL_BODY, ROOT_REPLY_BODY, ROOT_ACCEPTED_REPLY, ROOT_ACCEPTED_STATUS,
+ ROOT_REJECTED_REPLY, ROOT_AUTH_ERROR, ROOT_AUTH_FLAVOR, ROOT_AUTH_UNIX_PARAMS, ROOT_OPAQUE) = range(11)
+ROOT_NAMES = ["RpcMessage", "MessageType", "CallBody", "ReplyBody", "AcceptedReply", "AcceptedStatus",
+              "RejectedReply", "AuthError", "AuthFlavor", "AuthUnixParams", "Opaque"]
+OPAQUE_ENCODE_MAX = 255
+OPAQUE_MAX_LEN = 0xFFFFFF
 
 ACCEPT = {"success": 0, "prog_unavail": 1, "prog_mismatch": 2, "proc_unavail": 3,
           "garbage_args": 4, "system_err": 5}

@@ -19,11 +19,11 @@ LIB_PATH = os.environ.get("ONC_RPC_AMD_LIB") or os.path.join(os.path.dirname(os.
 
 K_NAMES = ["enc_len_kernel", "scan_tiles_kernel", "enc_emit_kernel", "decode_kernel",
            "len_tiles_kernel", "len_apply_kernel", "iov_len_kernel", "iov_emit_kernel",
-           "frame_chunks_kernel", "frame_write_kernel", "frame_coff_kernel", "frame_walk_kernel",
+           "frame_chunks_kernel", "frame_write_kernel", "frame_walk_kernel",
            "frame_counts_kernel", "frame_guess_kernel"]
 (K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY, K_IOV_LEN,
- K_IOV_EMIT, K_FRAME, K_FRAME_WRITE, K_FRAME_OFFSETS, K_FRAME_WALK, K_FRAME_COUNTS, K_FRAME_GUESS) = range(14)
-ABI_VERSION = 3
+ K_IOV_EMIT, K_FRAME, K_FRAME_WRITE, K_FRAME_WALK, K_FRAME_COUNTS, K_FRAME_GUESS) = range(13)
+ABI_VERSION = 4
 K_COUNT = len(K_NAMES)
 
 # every symbol include/onc_rpc.h declares
@@ -33,7 +33,7 @@ EXPORTED = [
     "onc_codec_enable_timing", "onc_codec_kernel_stats", "onc_codec_reset_stats",
     "onc_kernel_name", "onc_encode_lengths", "onc_encode", "onc_decode", "onc_scan_lengths",
     "onc_expected_message_len", "onc_encode_iov", "onc_frame_stream", "onc_encode_plan", "onc_encode_emit",
-    "onc_decode_lengths",
+    "onc_decode_lengths", "onc_decode_body", "onc_encode_body", "onc_encode_body_lengths",
 ]
 
 
@@ -87,8 +87,16 @@ def load_library(path=LIB_PATH):
     lib.onc_encode_iov.argtypes = [vp, C.POINTER(OncBatch), vp, u64, vp, vp, vp]
     lib.onc_expected_message_len.argtypes = [C.c_char_p, u64, C.POINTER(C.c_uint32)]
     lib.onc_expected_message_len.restype = C.c_int32
+    lib.onc_decode_body.argtypes = [vp, i32, vp, vp, u64, i32, vp, C.POINTER(OncDecoded), vp]
+    lib.onc_encode_body.argtypes = [vp, i32, C.POINTER(OncBatch), vp, u64, vp, vp, vp]
+    lib.onc_encode_body_lengths.argtypes = [vp, i32, C.POINTER(OncBatch), vp, vp]
     for name in EXPORTED:
         getattr(lib, name).restype = getattr(lib, name).restype or i32
+    # a stale library would read a differently laid out onc_batch and label
+    # the kernel timings wrongly: refuse it
+    abi = lib.onc_abi_version()
+    if abi != ABI_VERSION:
+        raise CodecError(f"{path}: ABI {abi}, this binding expects {ABI_VERSION} (rebuild: __graft_entry__.build())")
     _LIB = lib
     return lib
 
@@ -257,6 +265,25 @@ class Codec:
                                                 _ptr(rec_off) if rec_off is not None else None, C.byref(d)),
                     "onc_decode_lengths")
 
+    # -- body-level roots (ONC_ROOT_*) ---------------------------------------
+    def decode_body(self, root, wire, rec_off, n, mode, msgs, unix, status, aux0, aux1, param=None, consumed=None):
+        """onc_decode_body: each record decoded as `root`'s TryFrom."""
+        d = OncDecoded(msgs.data_ptr(), unix.data_ptr(), status.data_ptr(), aux0.data_ptr(),
+                       aux1.data_ptr())
+        self._check(self.lib.onc_decode_body(self.h, root, _ptr(wire), _ptr(rec_off), n, mode, _ptr(param),
+                                             C.byref(d), _ptr(consumed)), "onc_decode_body")
+
+    def encode_body_lengths(self, root, batch: DeviceBatch, rec_len, status):
+        b = batch.c_struct()
+        self._check(self.lib.onc_encode_body_lengths(self.h, root, C.byref(b), _ptr(rec_len), _ptr(status)),
+                    "onc_encode_body_lengths")
+
+    def encode_body(self, root, batch: DeviceBatch, out, rec_off, status, rec_len=None, out_cap=None):
+        b = batch.c_struct()
+        cap = out.numel() if out_cap is None else out_cap
+        self._check(self.lib.onc_encode_body(self.h, root, C.byref(b), _ptr(out), cap, _ptr(rec_off), _ptr(status),
+                                             _ptr(rec_len)), "onc_encode_body")
+
     def scan_lengths(self, rec_len, n, base, rec_off):
         self._check(self.lib.onc_scan_lengths(self.h, _ptr(rec_len), n, base, _ptr(rec_off)),
                     "onc_scan_lengths")
@@ -337,3 +364,39 @@ def decode_host_wire(codec: Codec, wire: np.ndarray, rec_off: np.ndarray, mode, 
     codec.decode(w, off, n, mode, bufs.msgs, bufs.unix, bufs.status, bufs.aux0, bufs.aux1)
     codec.sync()
     return bufs.to_host()
+
+
+def encode_body_host_batch(codec: Codec, root, hb: L.HostBatch, device="cuda", out_cap=None):
+    """Convenience: host batch -> GPU onc_encode_body -> (wire bytes, rec_off, status, rec_len) on host."""
+    torch = _torch()
+    db = DeviceBatch.from_host(hb, device)
+    n = hb.n
+    rec_len = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    status = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    if n:
+        codec.encode_body_lengths(root, db, rec_len, status)
+        codec.sync()
+    total = int(rec_len.cpu().numpy().view(np.uint32)[:n].astype(np.uint64).sum())
+    cap = total if out_cap is None else out_cap
+    out = torch.zeros(max(16, (cap + 15) // 16 * 16), dtype=torch.uint8, device=device)
+    rec_off = torch.empty(n + 1, dtype=torch.int64, device=device)
+    codec.encode_body(root, db, out, rec_off, status, rec_len, out_cap=cap)
+    codec.sync()
+    return (out.cpu().numpy()[:min(total, cap)].tobytes(), rec_off.cpu().numpy().view(np.uint64).copy(),
+            status.cpu().numpy()[:n].copy(), rec_len.cpu().numpy().view(np.uint32)[:n].copy())
+
+
+def decode_body_host_wire(codec: Codec, root, wire: np.ndarray, rec_off: np.ndarray, mode, param=None, device="cuda"):
+    """Convenience: packed records + offsets (host) -> GPU onc_decode_body ->
+    (msgs, unix, status, aux0, aux1, consumed) on host."""
+    torch = _torch()
+    n = len(rec_off) - 1
+    w = to_device(wire, device)
+    off = torch.from_numpy(rec_off.astype(np.uint64).view(np.int64).copy()).to(device)
+    bufs = DecodeBuffers(n, device)
+    prm = None if param is None else torch.from_numpy(np.asarray(param, np.uint32).view(np.int32).copy()).to(device)
+    consumed = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    codec.decode_body(root, w, off, n, mode, bufs.msgs, bufs.unix, bufs.status, bufs.aux0, bufs.aux1,
+                      param=prm, consumed=consumed)
+    codec.sync()
+    return bufs.to_host() + (consumed.cpu().numpy().view(np.uint32)[:n].copy(),)

@@ -1209,3 +1209,297 @@ int32_t oracle_opaque_encode(const uint8_t* body, uint32_t len, uint8_t* out, ui
     *written = w.pos;
     return e.code;
 }
+
+/* ---------------------------------------------------------------------- */
+/* Body-level roots (ONC_ROOT_*): each type's own TryFrom / serialise_into */
+/* ---------------------------------------------------------------------- */
+
+/* AuthError::try_from(Bytes) — rejected_reply.rs:215-236 */
+static o_err auth_error_try_from_bytes(o_bytes v, uint32_t* e) {
+    uint32_t x;
+    TRY(bytes_try_u32(&v, &x));
+    if (x > ONC_AUTH_STAT_MAX) return o_error(ONC_ERR_INVALID_AUTH_ERROR, x, 0);
+    *e = x;
+    return O_OK;
+}
+
+/* AcceptedReply::from_cursor — accepted_reply.rs:35-40 */
+static o_err accepted_reply_from_cursor(o_cursor* c, o_accepted_reply* r) {
+    TRY(auth_from_cursor(c, &r->verf));
+    return accepted_status_from_cursor(c, &r->status);
+}
+
+/* AcceptedReply::try_from(Bytes) — accepted_reply.rs:92-104 */
+static o_err accepted_reply_try_from_bytes(o_bytes v, o_accepted_reply* r) {
+    TRY(auth_try_from_bytes(v, &r->verf));
+    bytes_advance(&v, auth_serialised_len(&r->verf));
+    return accepted_status_try_from_bytes(v, &r->status);
+}
+
+/* The decoded value of a root as a descriptor (include/onc_rpc.h "Descriptor
+ * shape of a root's value"); *consumed = the value's serialised_len(). */
+int32_t oracle_decode_body(int root, const uint8_t* base, const uint8_t* buf, uint64_t len, int mode,
+                           uint32_t param, uint64_t unix_slot_base, onc_msg* msg, onc_unix_params unix[2],
+                           uint32_t* aux0, uint32_t* aux1, uint32_t* consumed) {
+    o_message m;
+    memset(&m, 0, sizeof(m));
+    memset(msg, 0, sizeof(*msg));
+    *consumed = 0;
+    *aux0 = *aux1 = 0;
+    if (root == ONC_ROOT_RPC_MESSAGE) {
+        int32_t st = oracle_decode_message(base, buf, len, mode, unix_slot_base, msg, unix, aux0, aux1);
+        if (st == ONC_OK) *consumed = (uint32_t)len;
+        return st;
+    }
+    const int bytes = mode == ONC_DECODE_BYTES;
+    o_cursor c = {buf, len, 0};
+    o_bytes v = {buf, len};
+    o_err e = O_OK;
+    uint64_t slen = 0;
+    /* the message-shaped roots fill m, then message_to_desc */
+    switch (root) {
+        case ONC_ROOT_MESSAGE_TYPE:
+            e = bytes ? message_type_try_from_bytes(v, &m) : message_type_from_cursor(&c, &m);
+            if (e.code == ONC_OK) slen = message_serialised_len(&m) - 8;
+            break;
+        case ONC_ROOT_CALL_BODY:
+            m.msg_type = ONC_MSG_CALL;
+            e = bytes ? call_try_from_bytes(v, &m.call) : call_from_cursor(&c, &m.call);
+            if (e.code == ONC_OK) slen = call_serialised_len(&m.call);
+            break;
+        case ONC_ROOT_REPLY_BODY:
+            m.msg_type = ONC_MSG_REPLY;
+            e = bytes ? reply_try_from_bytes(v, &m.reply) : reply_from_cursor(&c, &m.reply);
+            if (e.code == ONC_OK) slen = reply_serialised_len(&m.reply);
+            break;
+        case ONC_ROOT_ACCEPTED_REPLY:
+            m.msg_type = ONC_MSG_REPLY;
+            m.reply.variant = ONC_REPLY_ACCEPTED;
+            e = bytes ? accepted_reply_try_from_bytes(v, &m.reply.accepted)
+                      : accepted_reply_from_cursor(&c, &m.reply.accepted);
+            /* AcceptedReply::serialised_len — accepted_reply.rs:64-66 */
+            if (e.code == ONC_OK)
+                slen = auth_serialised_len(&m.reply.accepted.verf) +
+                       accepted_status_serialised_len(&m.reply.accepted.status);
+            break;
+        case ONC_ROOT_ACCEPTED_STATUS:
+            m.msg_type = ONC_MSG_REPLY;
+            m.reply.variant = ONC_REPLY_ACCEPTED;
+            e = bytes ? accepted_status_try_from_bytes(v, &m.reply.accepted.status)
+                      : accepted_status_from_cursor(&c, &m.reply.accepted.status);
+            if (e.code == ONC_OK) slen = accepted_status_serialised_len(&m.reply.accepted.status);
+            break;
+        case ONC_ROOT_REJECTED_REPLY:
+            m.msg_type = ONC_MSG_REPLY;
+            m.reply.variant = ONC_REPLY_DENIED;
+            e = bytes ? rejected_try_from_bytes(v, &m.reply.denied) : rejected_from_cursor(&c, &m.reply.denied);
+            if (e.code == ONC_OK) slen = rejected_serialised_len(&m.reply.denied);
+            break;
+        case ONC_ROOT_AUTH_ERROR:
+            m.msg_type = ONC_MSG_REPLY;
+            m.reply.variant = ONC_REPLY_DENIED;
+            m.reply.denied.variant = ONC_REJECT_AUTH_ERROR;
+            e = bytes ? auth_error_try_from_bytes(v, &m.reply.denied.auth_error)
+                      : auth_error_from_cursor(&c, &m.reply.denied.auth_error);
+            if (e.code == ONC_OK) slen = 4; /* AuthError::serialised_len rejected_reply.rs:210-212 */
+            break;
+        case ONC_ROOT_AUTH_FLAVOR:
+        case ONC_ROOT_AUTH_UNIX_PARAMS:
+        case ONC_ROOT_OPAQUE: {
+            o_auth a;
+            memset(&a, 0, sizeof(a));
+            if (root == ONC_ROOT_AUTH_FLAVOR) {
+                e = bytes ? auth_try_from_bytes(v, &a) : auth_from_cursor(&c, &a);
+                if (e.code == ONC_OK) slen = auth_serialised_len(&a);
+            } else if (root == ONC_ROOT_AUTH_UNIX_PARAMS) {
+                a.kind = O_AUTH_UNIX;
+                e = bytes ? unix_try_from_bytes(v, &a.unix) : unix_from_cursor(&c, param, &a.unix);
+                if (e.code == ONC_OK) slen = unix_serialised_len(&a.unix);
+            } else {
+                /* the descriptor's 24-bit length bounds max_len (onc_rpc.h ONC_OPAQUE_MAX_LEN) */
+                uint64_t max_len = param < ONC_OPAQUE_MAX_LEN ? param : ONC_OPAQUE_MAX_LEN;
+                o_bytes body;
+                if (bytes) {
+                    e = bytes_try_array(&v, max_len, &body);
+                } else {
+                    o_slice s;
+                    e = opaque_from_wire(&c, max_len, &s);
+                    body.ptr = s.ptr;
+                    body.len = s.len;
+                }
+                a.kind = O_AUTH_NONE;
+                if (e.code == ONC_OK) {
+                    a.data.ptr = body.ptr;
+                    a.data.len = body.len;
+                    slen = opaque_serialised_len(body.len);
+                }
+            }
+            *aux0 = e.a0;
+            *aux1 = e.a1;
+            if (e.code != ONC_OK) return e.code;
+            msg->msg_type = ONC_MSG_CALL;
+            auth_to_desc(&a, base, unix_slot_base, &msg->cred, &unix[0]);
+            if (root == ONC_ROOT_AUTH_UNIX_PARAMS) msg->cred.id = ONC_AUTH_UNIX;
+            *consumed = (uint32_t)slen;
+            return ONC_OK;
+        }
+        default:
+            return ONC_RC_EINVAL;
+    }
+    *aux0 = e.a0;
+    *aux1 = e.a1;
+    if (e.code != ONC_OK) return e.code;
+    message_to_desc(&m, base, unix_slot_base, msg, unix);
+    if (root == ONC_ROOT_ACCEPTED_STATUS) memset(&msg->verf, 0, sizeof(msg->verf));   /* no verifier in the value */
+    *consumed = (uint32_t)slen;
+    return ONC_OK;
+}
+
+/* Shape check of a descriptor for `root` (include/onc_rpc.h). */
+static int root_shape_ok(const onc_msg* d, int root) {
+    int call = d->msg_type == ONC_MSG_CALL, reply = d->msg_type == ONC_MSG_REPLY;
+    int acc = reply && d->reply_stat == ONC_REPLY_ACCEPTED, den = reply && d->reply_stat == ONC_REPLY_DENIED;
+    uint32_t ck = ONC_AUTH_KIND(d->cred), cl = ONC_AUTH_LEN(d->cred);
+    switch (root) {
+        case ONC_ROOT_MESSAGE_TYPE: return call || reply;
+        case ONC_ROOT_CALL_BODY:
+        case ONC_ROOT_AUTH_FLAVOR: return call;
+        case ONC_ROOT_AUTH_UNIX_PARAMS: return call && ck == ONC_KIND_UNIX;
+        case ONC_ROOT_OPAQUE: return call && ck != ONC_KIND_UNIX && ck <= ONC_KIND_UNKNOWN && cl <= ONC_OPAQUE_ENCODE_MAX;
+        case ONC_ROOT_REPLY_BODY: return reply;
+        case ONC_ROOT_ACCEPTED_REPLY:
+        case ONC_ROOT_ACCEPTED_STATUS: return acc;
+        case ONC_ROOT_REJECTED_REPLY: return den;
+        case ONC_ROOT_AUTH_ERROR: return den && d->stat == ONC_REJECT_AUTH_ERROR;
+        default: return 0;
+    }
+}
+
+/* `root`::serialise_into of a descriptor (include/onc_rpc.h
+ * onc_encode_body_lengths for the checks and their order). */
+int32_t oracle_encode_body(int root, const onc_msg* msg, const onc_unix_params* unix_table,
+                           const uint8_t* auth_arena, const uint8_t* payload_arena, uint8_t* out, uint64_t cap,
+                           uint64_t* written, uint64_t* serialised_len) {
+    *written = 0;
+    *serialised_len = 0;
+    if (root == ONC_ROOT_RPC_MESSAGE)
+        return oracle_encode_message(msg, unix_table, auth_arena, payload_arena, out, cap, written, serialised_len);
+    if (!root_shape_ok(msg, root)) return ONC_ENC_BAD_DESCRIPTOR;
+    o_message m;
+    o_auth a;
+    uint64_t slen = 0, assoc = 0, assoc2 = 0;
+    o_err e = O_OK;
+    if (root == ONC_ROOT_AUTH_FLAVOR || root == ONC_ROOT_AUTH_UNIX_PARAMS || root == ONC_ROOT_OPAQUE) {
+        e = auth_from_desc(&msg->cred, unix_table, auth_arena, &a);
+        if (e.code != ONC_OK) return e.code;
+        if (root == ONC_ROOT_AUTH_FLAVOR) {
+            slen = auth_serialised_len(&a);
+            assoc = auth_associated_data_len(&a);
+        } else if (root == ONC_ROOT_AUTH_UNIX_PARAMS) {
+            slen = unix_serialised_len(&a.unix);
+        } else {
+            slen = opaque_serialised_len(a.data.len);
+        }
+    } else if (root == ONC_ROOT_ACCEPTED_STATUS) {
+        /* only the status is serialised: the verifier is not read */
+        if (msg->stat > ONC_ACCEPT_SYSTEM_ERR) return ONC_ENC_BAD_DESCRIPTOR;
+        memset(&m, 0, sizeof(m));
+        m.reply.accepted.status.variant = msg->stat;
+        m.reply.accepted.status.low = msg->u.mismatch.low;
+        m.reply.accepted.status.high = msg->u.mismatch.high;
+        m.reply.accepted.status.payload.ptr = payload_arena + msg->payload_off;
+        m.reply.accepted.status.payload.len = msg->payload_len;
+        slen = accepted_status_serialised_len(&m.reply.accepted.status);
+    } else {
+        e = message_from_desc(msg, unix_table, auth_arena, payload_arena, &m);
+        if (e.code != ONC_OK) return e.code;
+        switch (root) {
+            case ONC_ROOT_MESSAGE_TYPE: slen = message_serialised_len(&m) - 8; break;
+            case ONC_ROOT_CALL_BODY: slen = call_serialised_len(&m.call); break;
+            case ONC_ROOT_REPLY_BODY: slen = reply_serialised_len(&m.reply); break;
+            case ONC_ROOT_ACCEPTED_REPLY:
+                slen = auth_serialised_len(&m.reply.accepted.verf) +
+                       accepted_status_serialised_len(&m.reply.accepted.status);
+                break;
+            case ONC_ROOT_REJECTED_REPLY: slen = rejected_serialised_len(&m.reply.denied); break;
+            default: slen = 4; break; /* AUTH_ERROR */
+        }
+        if (m.msg_type == ONC_MSG_CALL) {
+            assoc = auth_associated_data_len(&m.call.cred);
+            assoc2 = auth_associated_data_len(&m.call.verf);
+        } else if (m.reply.variant == ONC_REPLY_ACCEPTED && root != ONC_ROOT_ACCEPTED_STATUS) {
+            assoc2 = auth_associated_data_len(&m.reply.accepted.verf);
+        }
+    }
+    if (slen & 0xFFFFFFFF80000000ull) return ONC_ENC_TOO_LONG;
+    if (assoc > ONC_MAX_AUTH_LEN || assoc2 > ONC_MAX_AUTH_LEN) return ONC_ENC_AUTH_GT_200;
+    *serialised_len = slen;
+    o_writer w = {out, cap, 0};
+    switch (root) {
+        case ONC_ROOT_MESSAGE_TYPE: /* MessageType::serialise_into rpc_message.rs:55-68 */
+            e = w_write_u32(&w, m.msg_type);
+            if (e.code == ONC_OK)
+                e = m.msg_type == ONC_MSG_CALL ? call_serialise_into(&w, &m.call) : reply_serialise_into(&w, &m.reply);
+            break;
+        case ONC_ROOT_CALL_BODY: e = call_serialise_into(&w, &m.call); break;
+        case ONC_ROOT_REPLY_BODY: e = reply_serialise_into(&w, &m.reply); break;
+        case ONC_ROOT_ACCEPTED_REPLY: /* AcceptedReply::serialise_into accepted_reply.rs:58-61 */
+            e = auth_serialise_into(&w, &m.reply.accepted.verf);
+            if (e.code == ONC_OK) e = accepted_status_serialise_into(&w, &m.reply.accepted.status);
+            break;
+        case ONC_ROOT_ACCEPTED_STATUS: e = accepted_status_serialise_into(&w, &m.reply.accepted.status); break;
+        case ONC_ROOT_REJECTED_REPLY: /* rejected_reply.rs:61-73 */
+            e = w_write_u32(&w, m.reply.denied.variant);
+            if (e.code == ONC_OK)
+                e = m.reply.denied.variant == ONC_REJECT_RPC_MISMATCH
+                        ? (w_write_u32(&w, m.reply.denied.low).code == ONC_OK ? w_write_u32(&w, m.reply.denied.high)
+                                                                              : o_error(ONC_ENC_WRITE_ZERO, 0, 0))
+                        : w_write_u32(&w, m.reply.denied.auth_error);
+            break;
+        case ONC_ROOT_AUTH_ERROR: e = w_write_u32(&w, m.reply.denied.auth_error); break;
+        case ONC_ROOT_AUTH_FLAVOR: e = auth_serialise_into(&w, &a); break;
+        case ONC_ROOT_AUTH_UNIX_PARAMS: e = unix_serialise_into(&w, &a.unix); break;
+        default: e = opaque_serialise_into(&w, a.data); break; /* OPAQUE */
+    }
+    *written = w.pos;
+    return e.code;
+}
+
+void oracle_encode_body_batch(int root, uint64_t n, const onc_msg* msgs, const onc_unix_params* unix_table,
+                              const uint8_t* auth_arena, const uint8_t* payload_arena, uint8_t* out,
+                              uint64_t out_cap, uint64_t* rec_off, int32_t* status, uint32_t* rec_len) {
+    uint64_t off = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t written, slen;
+        uint64_t cap = out_cap > off ? out_cap - off : 0;
+        int32_t st = oracle_encode_body(root, &msgs[i], unix_table, auth_arena, payload_arena, cap ? out + off : out,
+                                        cap, &written, &slen);
+        uint64_t len = (st == ONC_OK || st == ONC_ENC_WRITE_ZERO) ? slen : 0;
+        if (rec_off) rec_off[i] = off;
+        if (status) status[i] = st;
+        if (rec_len) rec_len[i] = (uint32_t)len;
+        off += len;
+    }
+    if (rec_off) rec_off[n] = off;
+}
+
+void oracle_decode_body_batch(int root, const uint8_t* wire, const uint64_t* rec_off, uint64_t n, int mode,
+                              const uint32_t* param, onc_msg* msgs, onc_unix_params* unix_params, int32_t* status,
+                              uint32_t* aux0, uint32_t* aux1, uint32_t* consumed) {
+    for (uint64_t i = 0; i < n; i++) {
+        onc_unix_params u[2];
+        memset(u, 0, sizeof(u));
+        uint64_t a = rec_off[i], b = rec_off[i + 1];
+        int32_t st = oracle_decode_body(root, wire, wire + a, b - a, mode, param ? param[i] : 0, 2 * i, &msgs[i], u,
+                                        &aux0[i], &aux1[i], &consumed[i]);
+        status[i] = st;
+        if (st == ONC_OK) {
+            int cred_unix = ONC_AUTH_KIND(msgs[i].cred) == ONC_KIND_UNIX && msgs[i].msg_type == ONC_MSG_CALL;
+            int verf_unix = ONC_AUTH_KIND(msgs[i].verf) == ONC_KIND_UNIX &&
+                            (msgs[i].msg_type == ONC_MSG_CALL || msgs[i].reply_stat == ONC_REPLY_ACCEPTED) &&
+                            root != ONC_ROOT_AUTH_FLAVOR && root != ONC_ROOT_AUTH_UNIX_PARAMS;
+            if (cred_unix) unix_params[2 * i] = u[0];
+            if (verf_unix) unix_params[2 * i + 1] = u[1];
+        }
+    }
+}

@@ -99,6 +99,25 @@ int32_t oracle_opaque_encode(const uint8_t* body, uint32_t len, uint8_t* out, ui
 /* pad_length (opaque.rs:115-121) */
 uint32_t oracle_pad_length(uint32_t l);
 
+/* Body-level roots (ONC_ROOT_*, include/onc_rpc.h): `root`'s own TryFrom over
+ * buf[0..len) (slice / Bytes), the descriptor shape of include/onc_rpc.h;
+ * *consumed = the decoded value's serialised_len(). param = expected_len
+ * (AUTH_UNIX_PARAMS, slice) / max_len (OPAQUE). */
+int32_t oracle_decode_body(int root, const uint8_t* base, const uint8_t* buf, uint64_t len, int mode,
+                           uint32_t param, uint64_t unix_slot_base, onc_msg* msg, onc_unix_params unix[2],
+                           uint32_t* aux0, uint32_t* aux1, uint32_t* consumed);
+/* `root`::serialise_into of a descriptor, with onc_encode_body_lengths' checks. */
+int32_t oracle_encode_body(int root, const onc_msg* msg, const onc_unix_params* unix_table,
+                           const uint8_t* auth_arena, const uint8_t* payload_arena, uint8_t* out, uint64_t cap,
+                           uint64_t* written, uint64_t* serialised_len);
+/* Batch forms (the caller's loop), layouts as onc_encode_body / onc_decode_body. */
+void oracle_encode_body_batch(int root, uint64_t n, const onc_msg* msgs, const onc_unix_params* unix_table,
+                              const uint8_t* auth_arena, const uint8_t* payload_arena, uint8_t* out,
+                              uint64_t out_cap, uint64_t* rec_off, int32_t* status, uint32_t* rec_len);
+void oracle_decode_body_batch(int root, const uint8_t* wire, const uint64_t* rec_off, uint64_t n, int mode,
+                              const uint32_t* param, onc_msg* msgs, onc_unix_params* unix_params, int32_t* status,
+                              uint32_t* aux0, uint32_t* aux1, uint32_t* consumed);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,6 +68,14 @@ def load():
     lib.oracle_opaque_encode.restype = C.c_int32
     lib.oracle_pad_length.argtypes = [u32]
     lib.oracle_pad_length.restype = u32
+    lib.oracle_decode_body.argtypes = [i32, vp, vp, u64, i32, u32, u64, vp, vp, vp, vp, vp]
+    lib.oracle_decode_body.restype = C.c_int32
+    lib.oracle_encode_body.argtypes = [i32, vp, vp, vp, vp, vp, u64, vp, vp]
+    lib.oracle_encode_body.restype = C.c_int32
+    lib.oracle_encode_body_batch.argtypes = [i32, u64, vp, vp, vp, vp, vp, u64, vp, vp, vp]
+    lib.oracle_encode_body_batch.restype = None
+    lib.oracle_decode_body_batch.argtypes = [i32, vp, vp, u64, i32, vp, vp, vp, vp, vp, vp, vp]
+    lib.oracle_decode_body_batch.restype = None
     _LIB = lib
     return lib
 
@@ -177,3 +185,42 @@ def encode_message(hb, i=0, cap=None):
     st = lib.oracle_encode_message(_p(m), _p(hb.unix), _p(hb.auth_arena), _p(hb.payload_arena), _p(out),
                                    cap, _p(written), _p(slen))
     return st, out[:int(written[0])].tobytes(), int(slen[0])
+
+
+def encode_body_batch(root, hb, out_cap=None):
+    """`root`::serialise_into of every descriptor (onc_encode_body's checker)
+    -> (wire bytes, rec_off u64[n+1], status i32[n], rec_len u32[n])."""
+    lib = load()
+    n = hb.n
+    rec_off = np.zeros(n + 1, np.uint64)
+    status = np.zeros(max(n, 1), np.int32)
+    rec_len = np.zeros(max(n, 1), np.uint32)
+    args = (_p(hb.msgs), _p(hb.unix), _p(hb.auth_arena), _p(hb.payload_arena))
+    if out_cap is None:
+        lib.oracle_encode_body_batch(root, n, *args, None, 0, _p(rec_off), _p(status), _p(rec_len))
+        out_cap = int(rec_off[n])
+    out = np.zeros(max(out_cap, 1), np.uint8)
+    lib.oracle_encode_body_batch(root, n, *args, _p(out), out_cap, _p(rec_off), _p(status), _p(rec_len))
+    total = min(int(rec_off[n]), out_cap)
+    return out[:total].tobytes(), rec_off, status[:n], rec_len[:n]
+
+
+def decode_body_batch(root, wire, rec_off, mode, param=None):
+    """`root`'s TryFrom of every record (onc_decode_body's checker)
+    -> (msgs, unix, status, aux0, aux1, consumed)."""
+    from importlib import import_module
+    L = import_module("onc_rpc_amd.layout")
+    lib = load()
+    n = len(rec_off) - 1
+    wire = np.ascontiguousarray(wire, dtype=np.uint8)
+    rec_off = np.ascontiguousarray(rec_off, dtype=np.uint64)
+    prm = None if param is None else np.ascontiguousarray(param, dtype=np.uint32)
+    msgs = np.zeros(max(n, 1), L.MSG_DTYPE)
+    unix = np.zeros(max(2 * n, 1), L.UNIX_DTYPE)
+    status = np.zeros(max(n, 1), np.int32)
+    aux0 = np.zeros(max(n, 1), np.uint32)
+    aux1 = np.zeros(max(n, 1), np.uint32)
+    consumed = np.zeros(max(n, 1), np.uint32)
+    lib.oracle_decode_body_batch(root, _p(wire), _p(rec_off), n, mode, _p(prm), _p(msgs), _p(unix), _p(status),
+                                 _p(aux0), _p(aux1), _p(consumed))
+    return msgs[:n], unix[:2 * n], status[:n], aux0[:n], aux1[:n], consumed[:n]

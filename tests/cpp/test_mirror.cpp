@@ -331,6 +331,138 @@ static void test_stream_framing(Codec& c) {
     CHECK(stop->buffer_len() == a.size() - 10 && stop->expected() == a.size());
 }
 
+// ---- body-level types (onc_decode_body / onc_encode_body) -----------------------
+
+// flavor.rs:232-266 test_auth_unix_unaligned_machinename, :268-320 test_auth_unix
+static void test_auth_unix_flavors(Codec& c) {
+    for (const char* name : {"auth_unix_unaligned_machine_name", "auth_unix_16gids"}) {
+        const std::vector<uint8_t> raw = fixture(name);
+        for (DecodeMode mode : {DecodeMode::Slice, DecodeMode::Bytes}) {
+            const AuthFlavor f = AuthFlavor::try_from(c, Bytes(raw), mode);
+            CHECK(f.serialised_len(c) == raw.size());
+            CHECK(f.id() == ONC_AUTH_UNIX);
+            CHECK(f.kind() == AuthFlavor::Kind::AuthUnix);
+            const bool unaligned = raw.size() == 44;
+            CHECK(f.associated_data_len() == (unaligned ? 27u : 92u - 4 - 4 - 4 - 4));
+            CHECK(f.unix_params().uid() == (unaligned ? 0u : 501u));
+            if (unaligned) CHECK(f.unix_params().machine_name_str() == "LAPTOP-1QQBPDGM");
+            else CHECK(f.unix_params().gids() == gids16());
+            std::vector<uint8_t> out;
+            f.serialise_into(c, out);
+            CHECK(out == raw);
+        }
+    }
+}
+
+// flavor.rs:322-344 test_auth_none, :346-368 test_auth_short, :370-393 test_auth_unknown
+static void test_auth_opaque_flavors(Codec& c) {
+    const std::pair<const char*, AuthFlavor::Kind> cases[] = {{"auth_none_with_data", AuthFlavor::Kind::AuthNone},
+                                                              {"auth_short", AuthFlavor::Kind::AuthShort},
+                                                              {"auth_unknown_255", AuthFlavor::Kind::Unknown}};
+    for (const auto& cs : cases) {
+        const std::vector<uint8_t> raw = fixture(cs.first);
+        for (DecodeMode mode : {DecodeMode::Slice, DecodeMode::Bytes}) {
+            const AuthFlavor f = AuthFlavor::try_from(c, Bytes(raw), mode);
+            CHECK(f.kind() == cs.second);
+            CHECK(f.serialised_len(c) == 92);
+            CHECK(f.id() == (cs.second == AuthFlavor::Kind::AuthNone    ? 0u
+                             : cs.second == AuthFlavor::Kind::AuthShort ? 2u
+                                                                        : 255u));
+            CHECK(f.associated_data_len() == 92 - 4 - 4);
+            CHECK(f.data().has_value() && f.data()->len == f.associated_data_len());
+            CHECK(f.data()->ptr == raw.data() + 8);     // borrowed
+            std::vector<uint8_t> out;
+            f.serialise_into(c, out);
+            CHECK(out == raw);
+        }
+    }
+}
+
+// unix_params.rs:287-344 test_serialise_deserialise / :381-435 (Bytes),
+// :346-379 test_empty / :437-471 (Bytes)
+static void test_auth_unix_params(Codec& c) {
+    const std::vector<uint8_t> raw16 = fixture("unix_params_16gids_84B");
+    const std::vector<uint8_t> raw1 = fixture("unix_params_1gid_24B");
+    const AuthUnixParams want16(0, Bytes(), 501, 20, gids16());
+    const AuthUnixParams want1(0, Bytes(), 0, 0, {0});
+    std::vector<uint8_t> out;
+    want16.serialise_into(c, out);
+    CHECK(out == raw16);
+    CHECK(want16.serialised_len(c) == 84);
+    out.clear();
+    want1.serialise_into(c, out);
+    CHECK(out == raw1);
+    CHECK(AuthUnixParams::from_cursor(c, Bytes(raw16), 84) == want16);
+    CHECK(AuthUnixParams::try_from(c, Bytes(raw16)) == want16);
+    CHECK(AuthUnixParams::from_cursor(c, Bytes(raw1), 24) == want1);
+    CHECK(AuthUnixParams::try_from(c, Bytes(raw1)) == want1);
+    // from_cursor checks the consumed length (unix_params.rs:117-119)
+    bool threw = false;
+    try {
+        (void)AuthUnixParams::from_cursor(c, Bytes(raw1), 28);
+    } catch (const Error& e) {
+        threw = e.code() == ONC_ERR_INVALID_AUTH_DATA;
+    }
+    CHECK(threw);
+}
+
+// The call and reply bodies of the whole-message vectors, each as its own
+// type: CallBody (call_body.rs:168-210), ReplyBody (reply_body.rs:76-98),
+// AcceptedReply / AcceptedStatus (accepted_reply.rs:79-105, :234-265).
+static void test_body_types(Codec& c) {
+    const std::vector<uint8_t> call = fixture("call_auth_unix_16gids_288B");
+    const std::vector<uint8_t> reply = fixture("reply_accepted_success_76B");
+    for (DecodeMode mode : {DecodeMode::Slice, DecodeMode::Bytes}) {
+        const RpcMessage m = RpcMessage::try_from(c, Bytes(call), mode);
+        const Bytes cb(call.data() + 12, call.size() - 12);
+        const CallBody b = CallBody::try_from(c, cb, mode);
+        CHECK(b == *m.call_body());
+        CHECK(b.serialised_len(c) == cb.len);
+        std::vector<uint8_t> out;
+        b.serialise_into(c, out);
+        CHECK(Bytes(out) == cb);
+        const MessageType t = MessageType::try_from(c, Bytes(call.data() + 8, call.size() - 8), mode);
+        CHECK(t == m.message());
+        CHECK(t.serialised_len(c) == call.size() - 8);
+
+        const RpcMessage r = RpcMessage::try_from(c, Bytes(reply), mode);
+        const Bytes rb(reply.data() + 12, reply.size() - 12);
+        const ReplyBody rbody = ReplyBody::try_from(c, rb, mode);
+        CHECK(rbody == *r.reply_body());
+        out.clear();
+        rbody.serialise_into(c, out);
+        CHECK(Bytes(out) == rb);
+        const AcceptedReply ar = AcceptedReply::try_from(c, Bytes(rb.ptr + 4, rb.len - 4), mode);
+        CHECK(ar == *r.reply_body()->accepted());
+        CHECK(ar.serialised_len(c) == rb.len - 4);
+        const AcceptedStatus as = AcceptedStatus::try_from(c, Bytes(rb.ptr + 12, rb.len - 12), mode);
+        CHECK(as.kind() == AcceptedStatus::Kind::Success && as.payload().len == 48);
+        out.clear();
+        as.serialise_into(c, out);
+        CHECK(Bytes(out) == Bytes(rb.ptr + 12, rb.len - 12));
+    }
+    // rejected replies and auth errors, built then parsed back
+    for (const RejectedReply& j : {RejectedReply::rpc_version_mismatch(2, 5), RejectedReply::auth_error(AuthError::TooWeak)}) {
+        std::vector<uint8_t> out;
+        j.serialise_into(c, out);
+        CHECK(out.size() == j.serialised_len(c));
+        CHECK(RejectedReply::try_from(c, Bytes(out)) == j);
+        CHECK(RejectedReply::try_from(c, Bytes(out), DecodeMode::Bytes) == j);
+    }
+    std::vector<uint8_t> e;
+    serialise_into(c, AuthError::InvalidResponseVerifier, e);
+    CHECK(e == (std::vector<uint8_t>{0, 0, 0, 6}));
+    CHECK(auth_error_try_from(c, Bytes(e)) == AuthError::InvalidResponseVerifier);
+    const std::vector<uint8_t> bad = {0, 0, 0, 8};
+    bool threw = false;
+    try {
+        (void)auth_error_try_from(c, Bytes(bad), DecodeMode::Bytes);
+    } catch (const Error& x) {
+        threw = x.code() == ONC_ERR_INVALID_AUTH_ERROR && x.value() == 8;
+    }
+    CHECK(threw);
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s vectors.json\n", argv[0]);
@@ -356,6 +488,10 @@ int main(int argc, char** argv) {
         {"test_expected_message_len", test_expected_message_len},
         {"test_batch_round_trip", test_batch_round_trip},
         {"test_stream_framing", test_stream_framing},
+        {"test_auth_unix_flavors", test_auth_unix_flavors},
+        {"test_auth_opaque_flavors", test_auth_opaque_flavors},
+        {"test_auth_unix_params", test_auth_unix_params},
+        {"test_body_types", test_body_types},
     };
     for (const auto& t : tests) {
         try {

@@ -1,0 +1,157 @@
+"""GPU tests, round 3: the plan / emit contract (a plan is discarded by any
+call that reuses the handle's scratch; emit must get the plan's status
+array), and payloads at the first and last byte of a tightly sized payload
+arena on both enc_emit kernels. Bit-exact against the CPU oracle."""
+import numpy as np
+import pytest
+
+import onc_rpc_amd.layout as L
+import onc_rpc_amd.synth as S
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def R():
+    import onc_rpc_amd.runtime as R
+    return R
+
+
+@pytest.fixture(scope="module")
+def codec(R):
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    c = R.Codec(0)
+    yield c
+    c.close()
+
+
+def _plan(R, codec, hb):
+    import torch
+    db = R.DeviceBatch.from_host(hb)
+    st = torch.empty(hb.n, dtype=torch.int32, device="cuda")
+    codec.encode_plan(db, st)
+    return db, st
+
+
+def test_plan_discarded_by_scratch_users(codec, R, oracle):
+    """plan(A), then any call that writes the handle's scratch (encode
+    lengths / encode / iov / decode_lengths / scan_lengths), then emit(A):
+    refused (EINVAL) instead of placing A by the other call's totals; a fresh
+    plan makes emit work again, bit-exact."""
+    import torch
+    hb = S.mixed(3000, seed=31, pmin=0, pmax=600, exotic=0.2)
+    other = S.call_none(5000, 64)
+    o_wire, o_off, o_st, _ = oracle.encode_batch(hb)
+    total = len(o_wire)
+    buf = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
+    off = torch.empty(hb.n + 1, dtype=torch.int64, device="cuda")
+    dbo = R.DeviceBatch.from_host(other)
+    rl = torch.empty(other.n, dtype=torch.int32, device="cuda")
+    sto = torch.empty(other.n, dtype=torch.int32, device="cuda")
+    wire_o, off_o, _, len_o = R.encode_host_batch(codec, other)
+    w_dev = R.to_device(np.frombuffer(wire_o + b"\0" * 16, np.uint8), "cuda")
+    lens = torch.from_numpy(len_o.view(np.int32).copy()).cuda()
+    dec = R.DecodeBuffers(other.n)
+    offs = torch.empty(other.n + 1, dtype=torch.int64, device="cuda")
+
+    def lengths():
+        codec.encode_lengths(dbo, rl, sto)
+
+    def decode_lengths():
+        codec.decode_lengths(w_dev, lens, other.n, 0, L.DECODE_SLICE, dec.msgs, dec.unix, dec.status, dec.aux0,
+                             dec.aux1)
+
+    def scan():
+        codec.scan_lengths(lens, other.n, 0, offs)
+
+    def iov():
+        hdr = torch.empty(other.n * 64, dtype=torch.uint8, device="cuda")
+        iv = torch.empty(other.n * 32, dtype=torch.uint8, device="cuda")
+        codec.encode_iov(dbo, hdr, iv, sto)
+
+    def encode_other():
+        R.encode_host_batch(codec, other)
+
+    for between in (lengths, decode_lengths, scan, iov, encode_other):
+        db, st = _plan(R, codec, hb)
+        between()
+        with pytest.raises(R.CodecError):
+            codec.encode_emit(db, buf, off, st, out_cap=total)
+    db, st = _plan(R, codec, hb)
+    codec.encode_emit(db, buf, off, st, out_cap=total)
+    codec.sync()
+    assert buf.cpu().numpy()[:total].tobytes() == o_wire
+    assert np.array_equal(off.cpu().numpy().view(np.uint64), o_off)
+    assert np.array_equal(st.cpu().numpy(), o_st)
+
+
+def test_emit_needs_the_plans_status_array(codec, R, oracle):
+    """emit only adds WRITE_ZERO to the plan's statuses, so it must be handed
+    the array the plan filled (onc_rpc.h onc_encode_emit)."""
+    import torch
+    hb = S.call_none(700, 100)
+    db, st = _plan(R, codec, hb)
+    other_st = torch.empty_like(st)
+    buf = torch.zeros(700 * 160, dtype=torch.uint8, device="cuda")
+    off = torch.empty(hb.n + 1, dtype=torch.int64, device="cuda")
+    with pytest.raises(R.CodecError):
+        codec.encode_emit(db, buf, off, other_st)
+    codec.encode_emit(db, buf, off, st)      # the plan is still there
+    codec.sync()
+    o_wire, o_off, _, _ = oracle.encode_batch(hb)
+    assert buf.cpu().numpy()[:len(o_wire)].tobytes() == o_wire
+
+
+@pytest.mark.parametrize("variant", [0x200, 0x400, 0x200 | 0x4000, 0x200 | 0x8000])
+@pytest.mark.parametrize("layout", ["first_last", "reversed"])
+def test_payloads_at_arena_edges(R, oracle, monkeypatch, variant, layout):
+    """Payloads starting at byte 0 and ending at the last byte of a payload
+    arena declared exactly as large as its payloads (and placed at the very
+    end of its tensor): the interior-span source check (encode.hip
+    ws_stage_span) must keep every load inside [0, payload_len); output
+    bit-exact on the wave-specialised kernel (0x200, with and without the
+    interior / full-interior paths) and the wave-per-tile one (0x400)."""
+    import torch
+    monkeypatch.setenv("ONC_RPC_VARIANT", str(variant))
+    codec = R.Codec(0)
+    try:
+        rng = np.random.default_rng(variant + (7 if layout == "reversed" else 0))
+        n = 3000
+        plens = rng.integers(16, 700, n)
+        plens[::5] = 4 * rng.integers(4, 170, len(plens[::5]))      # word-path tiles too
+        msgs = []
+        for i in range(n):
+            msgs.append({"xid": i, "type": "call", "program": 100003, "program_version": 4, "procedure": 1,
+                         "cred": {"kind": "none", "data": None}, "verf": {"kind": "none", "data": None},
+                         "payload": rng.bytes(int(plens[i])).hex()})
+        hb = L.build_batch(msgs)
+        total_p = int(plens.sum())
+        arena = hb.payload_arena[:total_p]                     # drop the builder's spare byte: exact size
+        if layout == "reversed":
+            # record i's payload sits where record n-1-i's did: the first record
+            # reads the arena's last bytes, the last record its first bytes
+            offs = np.concatenate([[0], np.cumsum(plens[::-1])])[:-1][::-1]
+            new = np.zeros(total_p, np.uint8)
+            for i in range(n):
+                new[offs[i]:offs[i] + plens[i]] = arena[hb.msgs["payload_off"][i]:hb.msgs["payload_off"][i] + plens[i]]
+            hb.msgs["payload_off"] = offs
+            arena = new
+        hb = L.HostBatch(hb.msgs, hb.unix, hb.auth_arena, arena)
+        o_wire, o_off, o_st, _ = oracle.encode_batch(hb)
+        # the arena at the end of its tensor, declared exactly
+        big = torch.full((total_p + 4096,), 0xEE, dtype=torch.uint8, device="cuda")
+        pay = big[4096:]
+        pay.copy_(torch.from_numpy(arena.copy()).cuda())
+        db = R.DeviceBatch(n, R.to_device(hb.msgs, "cuda"), R.to_device(hb.unix, "cuda"),
+                           R.to_device(hb.auth_arena, "cuda"), pay, payload_len=total_p)
+        out = torch.zeros(len(o_wire) + 64, dtype=torch.uint8, device="cuda")
+        off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        st = torch.empty(n, dtype=torch.int32, device="cuda")
+        codec.encode(db, out, off, st, out_cap=len(o_wire))
+        codec.sync()
+        assert np.array_equal(st.cpu().numpy(), o_st) and (o_st == 0).all()
+        assert np.array_equal(off.cpu().numpy().view(np.uint64), o_off)
+        assert out.cpu().numpy()[:len(o_wire)].tobytes() == o_wire
+    finally:
+        codec.close()
