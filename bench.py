@@ -81,6 +81,8 @@ def parse(argv=None):
     ap.add_argument("--pcie-chunks", type=int, default=8,
                     help="record chunks of the pipelined PCIe-inclusive leg (two streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-check-records", type=int, default=0,
+                    help="--check-launch only: rehearse the closing CPU-baseline step on this many records")
     ap.add_argument("--no-pcie", action="store_true")
     ap.add_argument("--traffic-json", default=None,
                     help="per-kernel PMC traffic (default: the newest profiles/traffic_rNN[_<workload>].json)")
@@ -108,7 +110,11 @@ def spawn_ranks(gpus, argv):
 
 def check_launch(args, world, rank):
     """--check-launch: the ranks rendezvous, all_gather (rank, pid) and rank 0
-    prints the world as the process group sees it. No GPU call."""
+    prints the world as the process group sees it. No GPU call. With
+    --cpu-seconds > 0 the line also goes through the same closing step as a
+    GPU run (finish(): rank 0 times the CPU baseline after every rank's legs,
+    the others at the barrier) on a small configs[1] sample whose "GPU wire"
+    is the oracle's own encoding (CPU-only rehearsal of the N > 1 path)."""
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -118,12 +124,25 @@ def check_launch(args, world, rank):
         outs = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
         dist.all_gather(outs, t)
         ranks = [[int(x) for x in o] for o in outs]
-        dist.destroy_process_group()
     else:
         ranks = [[0, os.getpid()]]
-    if rank == 0:
-        print(json.dumps({"check_launch": True, "n_gpus": world, "gpus_arg": args.gpus, "ranks": ranks,
-                          "backend": args.backend if world > 1 else None}), flush=True)
+        dist = None
+    result = {"check_launch": True, "n_gpus": world, "gpus_arg": args.gpus, "ranks": ranks,
+              "backend": args.backend if world > 1 else None}
+    pending = None
+    if rank == 0 and args.cpu_check_records:
+        import numpy as np
+        import _onc_pkg
+        _onc_pkg.load()
+        import onc_rpc_amd.synth as S
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_ffi
+        hb = S.call_none(args.cpu_check_records, 256, seed=1)
+        wire, off, _, _ = oracle_ffi.encode_batch(hb)
+        pending = ("c1", hb, wire, np.frombuffer(wire + b"\0" * 16, np.uint8), off, 0)
+    finish(args, result, pending, dist, rank, world)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 # ---------------------------------------------------------------------------
@@ -651,6 +670,7 @@ def run_c4(args, torch, R, S, SH, L, dist, rank, world, local_rank, total, mode,
     ok = int((enc_status[:n] != 0).sum()) == 0 and int((dec.status[:n] != 0).sum()) == 0
     enc_total = int(rec_off[n]) if n else 0
     ok = ok and enc_total == local_bytes
+    ok = ok and c4_wire_bytes_ok(torch, out, db, lo, n)
     xid = dec.msgs.view(-1, 64)[:n, 0:4].contiguous().view(torch.int32).view(-1)
     want = (torch.arange(lo, hi, dtype=torch.int64, device=dev) & 0xFFFFFFFF).to(torch.int32)
     ok = ok and torch.equal(xid, want)
@@ -692,6 +712,32 @@ def run_c4(args, torch, R, S, SH, L, dist, rank, world, local_rank, total, mode,
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return res
+
+
+def c4_wire_bytes_ok(torch, out, db, lo, n, chunk=1 << 22):
+    """Every byte of a configs[4] shard's wire, on the device: record i is the
+    44-byte header of Call(xid lo + i, prog 100003, vers 4, proc 1,
+    AuthNone(None) x2) with record mark (300 - 4) | 1 << 31
+    (rpc_message.rs:136-164 with call_body.rs:98-108, flavor.rs:119-122), then
+    its 256 payload bytes from the arena (call_body.rs:107). Chunked, so the
+    comparison temporaries stay at a few GB."""
+    import numpy as np
+    words = [0x80000000 | (C4_W - 4), 0, 0, 2, 100003, 4, 1, 0, 0, 0, 0]
+    tmpl = torch.from_numpy(np.array(words, ">u4").view(np.uint8).copy()).to(out.device)
+    wire = out[: n * C4_W].view(n, C4_W)
+    pay = db.payload_arena[: n * 256].view(n, 256)
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        w = wire[a:b]
+        if not torch.equal(w[:, 44:], pay[a:b]):
+            return False
+        if not torch.equal(w[:, :4], tmpl[:4].expand(b - a, 4)) or not torch.equal(w[:, 8:44], tmpl[8:44].expand(b - a, 36)):
+            return False
+        x = torch.arange(lo + a, lo + b, dtype=torch.int64, device=out.device) & 0xFFFFFFFF
+        xb = torch.stack([(x >> s_) & 0xFF for s_ in (24, 16, 8, 0)], 1).to(torch.uint8)
+        if not torch.equal(w[:, 4:8], xb):
+            return False
+    return True
 
 
 def validate_iov(torch, n, iov, hdr_out, iov_tot, iov_status, wire, rec_off, hdr_len_ref, plen, hb, total_bytes,
@@ -932,11 +978,16 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
         result["config"]["header_bytes_per_gpu"] = sum_H
         result["config"].pop("parsed_bytes_per_gpu", None)
         result["config"].pop("decode_mode", None)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.iov:
+    if rank == 0 and not args.no_cpu_baseline and not args.iov:
         prefix = out[: min(total_bytes, 20_000 * 4300)].cpu().numpy().tobytes()
         wire_np = out.cpu().numpy()
         off_np = dec_off.cpu().numpy().view(np.uint64)
-        result["cpu_baseline"] = cpu_baseline(args, wl, hb, prefix, wire_np, off_np, mode)
+        if world == 1:
+            result["cpu_baseline"] = cpu_baseline(args, wl, hb, prefix, wire_np, off_np, mode)
+        else:
+            # N > 1: rank 0 times it after every GPU leg of every rank (main()),
+            # so no rank's timed region shares the host with it
+            result["_cpu_pending"] = (wl, hb, prefix, wire_np, off_np, mode)
     elif rank == 0:
         result["cpu_baseline"] = None
     codec.close()
@@ -944,6 +995,25 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return result
+
+
+def finish(args, result, pending, dist, rank, world):
+    """Closing step of every run: with N > 1 ranks, rank 0 times the CPU
+    baseline (`pending`: the arguments cpu_baseline needs) only after every
+    rank's GPU legs are done — no timed region shares the host with it —
+    then rank 0 prints the one JSON line."""
+    if dist is not None:
+        dist.barrier()                  # every rank's GPU legs are done
+    if pending is not None:
+        cb = cpu_baseline(args, *pending)
+        if world > 1:
+            cb["note"] = (f"timed on rank 0 after all {world} ranks finished their GPU legs (the other ranks "
+                          f"wait at the closing barrier); rank 0's shard of the same workload")
+        result["cpu_baseline"] = cb
+    if dist is not None:
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
 
 
 def main():
@@ -1008,8 +1078,7 @@ def main():
         if args.c4_leg == "on":
             result["configs4"] = run_c4(args, torch, R, S, SH, L, dist, rank, world, local_rank,
                                         args.c4_records, mode, args.steps, args.warmup)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+    finish(args, result, result.pop("_cpu_pending", None) if rank == 0 else None, dist, rank, world)
     if dist is not None:
         dist.destroy_process_group()
     if not ok:

@@ -120,22 +120,6 @@ struct Rules {
 // verifier (slot 2i + 1, k = 1), held in registers until the record is
 // parsed, then written out (see the end of decode_kernel): 24 words per
 // slot in onc_unix_params order.
-#ifdef ONC_DEC_LEAN
-// Lab: slots stored as soon as they are parsed (no registers held).
-struct UnixSlots {
-    onc_unix_params* out;
-    uint32_t mask;
-};
-__device__ __forceinline__ void put_unix(UnixSlots& us, uint64_t slot, uint32_t stamp, uint32_t uid, uint32_t gid,
-                                         uint32_t ng, uint64_t name_off, uint32_t nl, const uint32_t* gids) {
-    uint4* d = reinterpret_cast<uint4*>(us.out + slot);
-    d[0] = make_uint4(stamp, uid, gid, ng);
-    d[1] = make_uint4(uint32_t(name_off), uint32_t(name_off >> 32), nl, 0u);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) d[2 + q] = make_uint4(gids[4 * q], gids[4 * q + 1], gids[4 * q + 2], gids[4 * q + 3]);
-    us.mask |= 1u << (slot & 1);
-}
-#else
 struct UnixSlots {
     uint32_t w[2][24];
     uint32_t mask;      // bit k: slot k holds parameters
@@ -155,7 +139,6 @@ __device__ __forceinline__ void put_unix(UnixSlots& us, uint64_t slot, uint32_t 
     for (int g = 0; g < 16; ++g) us.w[k][8 + g] = gids[g];
     us.mask |= 1u << k;
 }
-#endif
 
 // One lane's slots straight to global memory (waves with few AUTH_UNIX
 // records), padded to whole 64-byte sectors: the credential slot with the
@@ -163,7 +146,6 @@ __device__ __forceinline__ void put_unix(UnixSlots& us, uint64_t slot, uint32_t 
 // the verifier slot with the credential slot's last 32 bytes zeroed (when
 // that one has none) — partial 64-byte sectors cost a read-modify-write
 // (c3 decode 537 -> 454 us with the padding).
-#ifndef ONC_DEC_LEAN
 __device__ __forceinline__ void put_unix_direct(onc_unix_params* pair, const UnixSlots& us) {
     uint4* d = reinterpret_cast<uint4*>(pair);          // 12 x 16 bytes: [cred 0..5][verf 6..11]
     if (us.mask & 1u) {
@@ -183,7 +165,6 @@ __device__ __forceinline__ void put_unix_direct(onc_unix_params* pair, const Uni
         for (int q = 0; q < 6; ++q) d[6 + q] = make_uint4(us.w[1][4 * q], us.w[1][4 * q + 1], us.w[1][4 * q + 2], us.w[1][4 * q + 3]);
     }
 }
-#endif
 
 // Slice mode AuthFlavor::from_cursor (flavor.rs:52-94) with
 // AuthUnixParams::from_cursor (unix_params.rs:90-129) and
@@ -684,9 +665,6 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     int32_t st = ONC_OK;
     UnixSlots us;
     us.mask = 0;
-#ifdef ONC_DEC_LEAN
-    us.out = a.out.unix_params;
-#endif
     uint32_t consumed = 0;
     if (valid) {
         if constexpr (kRoot) {
@@ -727,7 +705,6 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     // instruction (configs[3] decode 473 us with them, 411 us staged with
     // every sector, 275 us with no slot stores at all). Otherwise each lane
     // writes its own.
-#ifndef ONC_DEC_LEAN
     const uint64_t um = __ballot(us.mask != 0);
     if (um) {
         static_assert(kDecTile == 64, "slot staging: one wave, two halves of 32 records");
@@ -770,7 +747,6 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
             put_unix_direct(a.out.unix_params + 2 * i, us);
         }
     }
-#endif
     uint4* stage = reinterpret_cast<uint4*>(s_win);
 #pragma unroll
     for (int k = 0; k < 4; ++k) stage[4 * t + k] = mz[k];

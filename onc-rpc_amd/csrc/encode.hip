@@ -218,10 +218,6 @@ struct ImgTile {
     uint8_t map[kMap2Cap];           // granule -> span record owning its first chunk
 };
 
-__device__ __forceinline__ uint32_t sel4(const u32x4_a4& x, uint32_t i) {
-    return i == 0 ? x.x : (i == 1 ? x.y : (i == 2 ? x.z : x.w));
-}
-
 // Header words of a record into the image at byte offset b (any alignment).
 // The image is zeroed per span and every record ORs its bytes in
 // (ds_or_b32): a dword shared with a neighbouring record (b & 3 != 0: the
@@ -250,12 +246,6 @@ struct ImgSink {
 // The rotation by `rot` dwords is two select stages on its bits (8 selects)
 // rather than a 4-way select per dword.
 __device__ __forceinline__ void merge_words(const u32x4_a4& X, const uint4& L, uint32_t sel, uint32_t v[4]) {
-#ifdef ONC_MERGE_SEL4
-    const uint32_t rot = sel >> 4;
-    const uint32_t h[4] = {L.x, L.y, L.z, L.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = (sel >> i) & 1 ? sel4(X, (i + rot) & 3) : h[i];
-#else
     const bool r1 = (sel >> 4) & 1u, r2 = (sel >> 5) & 1u;
     const uint32_t a0 = r1 ? X.y : X.x, a1 = r1 ? X.z : X.y, a2 = r1 ? X.w : X.z, a3 = r1 ? X.x : X.w;
     const uint32_t z0 = r2 ? a2 : a0, z1 = r2 ? a3 : a1, z2 = r2 ? a0 : a2, z3 = r2 ? a1 : a3;
@@ -263,7 +253,6 @@ __device__ __forceinline__ void merge_words(const u32x4_a4& X, const uint4& L, u
     v[1] = sel & 2u ? z1 : L.y;
     v[2] = sel & 4u ? z2 : L.z;
     v[3] = sel & 8u ? z3 : L.w;
-#endif
 }
 
 // One chunk of the byte path: bytes [lo, hi) of the chunk are payload, taken
@@ -319,16 +308,10 @@ __device__ __forceinline__ ChunkPlan plan_chunk(const ImgTile& T, uint32_t gsh, 
         const uint32_t hi = hasp ? min(q.y - o, 16u) : 0u;
         P.sel = ((o - x) & 15u) | (lo << 8) | (hi << 16);
     } else {
-#ifdef ONC_MERGE_SEL4
-        uint32_t pm = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pm |= (o + 4 * i >= q.x && o + 4 * i < q.y) ? (1u << i) : 0u;
-#else
         // dwords i with o + 4i in [q.x, q.y) (word path: q.x, q.y, o all 4-aligned)
         const uint32_t lo = min(max(int32_t(q.x - o), 0), 16) >> 2;
         const uint32_t hi = min(max(int32_t(q.y - o), 0), 16) >> 2;
         const uint32_t pm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-#endif
         P.sel = (hasp ? pm : 0u) | (((o - x) >> 2) & 3u) << 4;
     }
     return P;
@@ -429,7 +412,7 @@ __device__ __forceinline__ void merge_chunk(const ChunkPlan& P, const uint32_t X
 // after the last step re-reads the last chunk). The one or two partial
 // chunks at the span's edges are written after the loop, with byte stores
 // of only the span's bytes.
-template <int kU, int kNT, bool kByte, int kPipe = 2>
+template <int kU, int kNT, bool kByte>
 __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, uint32_t gsh, uint64_t B0,
                                             uint64_t S0, uint64_t E, int32_t NCe, uintptr_t dummy) {
     const int lane = threadIdx.x & 63;
@@ -455,34 +438,14 @@ __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, 
         if (kNT & 2) __builtin_nontemporal_store(u32x4{v[0], v[1], v[2], v[3]}, d);  \
         else *d = u32x4{v[0], v[1], v[2], v[3]};                                          \
     }
-        if constexpr (kPipe == 3) {
-            // three register sets: two steps' loads in flight while one is consumed
-            ChunkPlan Pc[kU];
-            uint32_t Xc[kU][4];
-            uint4 Lc[kU];
-            ONC_ISSUE(Pa, Xa, La, cf);
-            ONC_ISSUE(Pb, Xb, Lb, cf + S);
-            for (int32_t st = cf;; st += 3 * S) {
-                ONC_ISSUE(Pc, Xc, Lc, st + 2 * S);
-                ONC_CONSUME(Pa, Xa, La, st);
-                if (st + S >= cl) break;
-                ONC_ISSUE(Pa, Xa, La, st + 3 * S);
-                ONC_CONSUME(Pb, Xb, Lb, st + S);
-                if (st + 2 * S >= cl) break;
-                ONC_ISSUE(Pb, Xb, Lb, st + 4 * S);
-                ONC_CONSUME(Pc, Xc, Lc, st + 2 * S);
-                if (st + 3 * S >= cl) break;
-            }
-        } else {
-            ONC_ISSUE(Pa, Xa, La, cf);
-            for (int32_t st = cf;; st += 2 * S) {
-                ONC_ISSUE(Pb, Xb, Lb, st + S);
-                ONC_CONSUME(Pa, Xa, La, st);
-                if (st + S >= cl) break;
-                ONC_ISSUE(Pa, Xa, La, st + 2 * S);
-                ONC_CONSUME(Pb, Xb, Lb, st + S);
-                if (st + 2 * S >= cl) break;
-            }
+        ONC_ISSUE(Pa, Xa, La, cf);
+        for (int32_t st = cf;; st += 2 * S) {
+            ONC_ISSUE(Pb, Xb, Lb, st + S);
+            ONC_CONSUME(Pa, Xa, La, st);
+            if (st + S >= cl) break;
+            ONC_ISSUE(Pa, Xa, La, st + 2 * S);
+            ONC_CONSUME(Pb, Xb, Lb, st + S);
+            if (st + 2 * S >= cl) break;
         }
 #undef ONC_ISSUE
 #undef ONC_CONSUME
@@ -504,7 +467,7 @@ __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, 
     }
 }
 
-template <int kU, int kNT, bool kFused, int kPipe = 2, bool kRoot = false>
+template <int kU, int kNT, bool kFused, bool kRoot = false>
 __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = tile * kEmitRecs;
@@ -621,7 +584,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                     // the header (bytes past its end read as zero)
                     const uintptr_t pb = sb + pst;
                     for (uint32_t k = 0; 4 * k < plen; ++k) w(load4_masked(pb + 4 * k, pb + plen));
-                } else if (kRoot && pst < (uint64_t(cfa) << 4)) {
+                } else if (kRoot && plen != 0 && pst < (uint64_t(cfa) << 4)) {
                     // a body root's header can be shorter than a chunk
                     // (AcceptedStatus: 4 bytes): payload bytes in the chunk
                     // the record starts in belong to a chunk the record
@@ -651,7 +614,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         if (E <= S0) continue;                         // no bytes (all records failed, or beyond out_cap)
         const int32_t NCe = int32_t(((E + 15) >> 4) - C0);
         if (byte_mode) stream_span<1, kNT, true>(a, T, gsh, B0, S0, E, NCe, dummy);
-        else stream_span<kU, kNT, false, kPipe>(a, T, gsh, B0, S0, E, NCe, dummy);
+        else stream_span<kU, kNT, false>(a, T, gsh, B0, S0, E, NCe, dummy);
         if (lo_rec == hi_rec && hi_rec == nrec) ONC_PROF(4);
     }
     ONC_PROF(5);
@@ -932,9 +895,6 @@ __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile
 #ifndef ONC_WS_U
 #define ONC_WS_U 2            // consumer chunks per lane per step (c1: 2 -> enc_emit 121 -> 116 us vs 1)
 #endif
-#ifndef ONC_WS_EVEN
-#define ONC_WS_EVEN 0   // 1: trim the grid to equal tiles per workgroup (977 for configs[1]): measured slower
-#endif
 constexpr int kWsGrid = 1024;   // persistent workgroups (4 per CU on 256 CUs)
 static_assert(kWsGrid / kTilesPerBlk <= 64, "a producer adds at most 64 workgroup totals per tile");
 
@@ -1019,15 +979,17 @@ __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
 // finds them cached, made the decode slower: 60 -> 69 us on c1, the dirty
 // lines are written back at the kernel boundary);
 // kOcc: workgroups per CU the register allocation must allow (0 = free)
-#ifndef ONC_EMIT_OCC
-#define ONC_EMIT_OCC 0   // lab: waves per SIMD the wave-per-tile kernel's registers must allow (0 = free: 106 VGPRs, 4)
-#endif
-template <int kU, int kNT = 0, int kOcc = 0, bool kFused = false, int kPipe = 2, bool kRoot = false>
-__global__ __launch_bounds__(64 * kFastWaves, kOcc ? kOcc * kFastWaves / 4 : 1) void enc_emit_kernel_t(EncArgs a) {
+// kNT: bit 0 = nontemporal payload loads, bit 1 = nontemporal stores (header
+// chunks stored temporally so that the decoder finds them cached made the
+// decode slower, 60 -> 69 us on c1: the dirty lines are written back at the
+// kernel boundary). Registers are left free (106 VGPRs, 4 waves per SIMD):
+// squeezed to 5 waves per SIMD every shape measured slower (spills).
+template <int kU, int kNT = 0, bool kFused = false, bool kRoot = false>
+__global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) {
     __shared__ ImgTile s_tiles[kFastWaves];
     const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
     if (tile < num_emit_tiles(a.n))
-        enc_emit_tile<kU, kNT, kFused, kPipe, kRoot>(a, s_tiles[threadIdx.x >> 6], tile);
+        enc_emit_tile<kU, kNT, kFused, kRoot>(a, s_tiles[threadIdx.x >> 6], tile);
 }
 
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
@@ -1041,8 +1003,9 @@ hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
 hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
     if (a.ws) {
         const uint64_t tiles = num_emit_tiles(a.n);
-        const uint64_t per = (tiles + kWsGrid - 1) / kWsGrid;
-        const uint32_t g = uint32_t(ONC_WS_EVEN ? (tiles + per - 1) / per : min(uint64_t(kWsGrid), tiles));
+        // (a grid trimmed to equal tiles per workgroup, 977 for configs[1],
+        // measured slower: concurrency beats the ragged last phase)
+        const uint32_t g = uint32_t(min(uint64_t(kWsGrid), tiles));
         if (a.ws == 2) ONC_LAUNCH((enc_emit_ws_kernel<1, kEmitNT>), dim3(g), dim3(256), 0, s, a);
         else ONC_LAUNCH((enc_emit_ws_kernel<ONC_WS_U, kEmitNT>), dim3(g), dim3(256), 0, s, a);
         return hipGetLastError();
@@ -1052,18 +1015,18 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
         // body-level roots (onc_encode_body): the wave-per-tile kernel with
         // the root switch (codec.hip never picks the wave-specialised one)
         if (a.fused_base)
-            ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, true, 2, true>), dim3(uint32_t(blocks)),
+            ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, true, true>), dim3(uint32_t(blocks)),
                        dim3(64 * kFastWaves), 0, s, a);
         else
-            ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, 0, false, 2, true>), dim3(uint32_t(blocks)),
+            ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false, true>), dim3(uint32_t(blocks)),
                        dim3(64 * kFastWaves), 0, s, a);
         return hipGetLastError();
     }
     if (a.fused_base)
-        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, ONC_EMIT_OCC, true>), dim3(uint32_t(blocks)),
+        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, true>), dim3(uint32_t(blocks)),
                            dim3(64 * kFastWaves), 0, s, a);
     else
-        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, ONC_EMIT_OCC, false>), dim3(uint32_t(blocks)),
+        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false>), dim3(uint32_t(blocks)),
                            dim3(64 * kFastWaves), 0, s, a);
     return hipGetLastError();
 }

@@ -134,7 +134,8 @@ def test_payloads_at_arena_edges(R, oracle, monkeypatch, variant, layout):
             offs = np.concatenate([[0], np.cumsum(plens[::-1])])[:-1][::-1]
             new = np.zeros(total_p, np.uint8)
             for i in range(n):
-                new[offs[i]:offs[i] + plens[i]] = arena[hb.msgs["payload_off"][i]:hb.msgs["payload_off"][i] + plens[i]]
+                o, src, ln = int(offs[i]), int(hb.msgs["payload_off"][i]), int(plens[i])
+                new[o:o + ln] = arena[src:src + ln]
             hb.msgs["payload_off"] = offs
             arena = new
         hb = L.HostBatch(hb.msgs, hb.unix, hb.auth_arena, arena)
@@ -155,3 +156,26 @@ def test_payloads_at_arena_edges(R, oracle, monkeypatch, variant, layout):
         assert out.cpu().numpy()[:len(o_wire)].tobytes() == o_wire
     finally:
         codec.close()
+
+
+def test_bench_two_ranks_line_has_cpu_baseline():
+    """A real 2-rank bench run (both ranks on GPU 0, gloo for the control
+    plane): the JSON line carries per-GPU rows, the aggregate, validated, and
+    the CPU baseline rank 0 timed after both ranks' GPU legs."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["ONC_BENCH_SAME_DEVICE"] = "1"
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--records", "20000", "--c4-leg", "off", "--iov-leg", "off", "--steps", "3", "--warmup", "1",
+                        "--cpu-seconds", "1", "--cpu-threads", "2", "--no-pcie"],
+                       env=env, cwd=root, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert r["n_gpus"] == 2 and r["validated"] and len(r["per_gpu"]) == 2
+    cb = r["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["sample_bit_exact_vs_gpu"] is True
+    assert "after all 2 ranks" in cb["note"]

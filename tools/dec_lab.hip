@@ -14,6 +14,9 @@
 #include <vector>
 
 #include "../onc-rpc_amd/csrc/decode.hip"
+namespace onc {
+thread_local LaunchEvents t_launch_events{nullptr, nullptr};   // the codec library defines it (codec.hip)
+}
 
 #define CK(x)                                                                                  \
     do {                                                                                       \
