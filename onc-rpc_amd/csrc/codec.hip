@@ -365,6 +365,10 @@ int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
     a.ws = ((c->variant & 0x200) || (!(c->variant & 0x400) && n && ws_shape)) ? (big ? 2u : 1u) : 0u;
     a.root = root;
     if (root != ONC_ROOT_RPC_MESSAGE) a.ws = 0;   // body roots: the wave-per-tile kernel
+    // the wave-specialised kernel checks the real payload volume itself
+    // (encode.hip ws_header_heavy): enc_len writes per-workgroup payload
+    // totals into the scratch's spare words
+    if (a.ws) a.block_pay = c->scratch + c->scratch_tiles;
     a.fused_base = (onc::num_len_blocks(n) <= onc::kFusedBlocks && !c->force_scan) || a.ws;
     return ONC_RC_OK;
 }

@@ -38,7 +38,7 @@ constexpr int kLenThreads = kLenRecs / kLenPer;
 // switch).
 template <bool kRoot>
 __global__ __launch_bounds__(kLenThreads) void enc_len_kernel(EncArgs a) {
-    __shared__ uint64_t s_wave[kLenThreads / 64];
+    __shared__ uint64_t s_wave[2 * (kLenThreads / 64)];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t rw = uint64_t(blockIdx.x) * kLenRecs + uint64_t(wv) * (64 * kLenPer);
     onc_msg d[kLenPer];
@@ -47,14 +47,15 @@ __global__ __launch_bounds__(kLenThreads) void enc_len_kernel(EncArgs a) {
         const uint64_t r = rw + 64 * k + lane;
         if (r < a.n) d[k] = a.msgs[r];
     }
-    uint64_t wsum = 0;
+    uint64_t wsum = 0, psum = 0;
 #pragma unroll
     for (int k = 0; k < kLenPer; ++k) {
         const uint64_t r = rw + 64 * k + lane;
-        uint64_t len = 0;
+        uint64_t len = 0, pay = 0;
         if (r < a.n) {
             const RecPlan p = kRoot ? plan_root(d[k], a.unix, a.bounds, a.root) : plan_record(d[k], a.unix, a.bounds);
             len = p.len;
+            pay = len - 4ull * meta_hw(p.meta);           // 0 for a failing record (len = meta = 0)
             a.status[r] = p.status;
             if (a.rec_len) a.rec_len[r] = uint32_t(len);
         }
@@ -62,13 +63,19 @@ __global__ __launch_bounds__(kLenThreads) void enc_len_kernel(EncArgs a) {
         const uint64_t tile = (rw + 64 * k) / kEmitRecs;
         if (lane == 63 && tile * kEmitRecs < a.n) a.tile_sum[tile] = incl;
         wsum += lane_u64(incl, 63);
+        if (a.block_pay) psum += lane_u64(wave_incl_scan_u64(pay), 63);
     }
     if (lane == 0) s_wave[wv] = wsum;
+    if (lane == 0 && a.block_pay) s_wave[kLenThreads / 64 + wv] = psum;
     __syncthreads();
     if (threadIdx.x < 64) {
         const uint64_t v = threadIdx.x < kLenThreads / 64 ? s_wave[threadIdx.x] : 0;
         const uint64_t t = wave_incl_scan_u64(v);
         if (threadIdx.x == 63) a.block_sum[blockIdx.x] = t;
+        if (a.block_pay) {
+            const uint64_t q = wave_incl_scan_u64(threadIdx.x < kLenThreads / 64 ? s_wave[kLenThreads / 64 + threadIdx.x] : 0);
+            if (threadIdx.x == 63) a.block_pay[blockIdx.x] = q;
+        }
     }
 }
 
@@ -107,8 +114,11 @@ struct TileLoads {
     uint64_t w[kW];
 };
 
-template <bool kFused>
-__device__ __forceinline__ TileLoads<kFused> tile_loads(const EncArgs& a, uint64_t tile) {
+// kGiven: the base of the tile's enc_len workgroup is the caller's
+// (`given`, the running sum of the wave-specialised kernel's header-heavy
+// mode) instead of a load of the scanned bases.
+template <bool kFused, bool kGiven = false>
+__device__ __forceinline__ TileLoads<kFused> tile_loads(const EncArgs& a, uint64_t tile, uint64_t given = 0) {
     const int lane = threadIdx.x & 63;
     const uint64_t blk = tile / (kLenRecs / kEmitRecs);
     const uint64_t t0 = blk * (kLenRecs / kEmitRecs);
@@ -119,7 +129,7 @@ __device__ __forceinline__ TileLoads<kFused> tile_loads(const EncArgs& a, uint64
 #pragma unroll
         for (int k = 0; k < TileLoads<kFused>::kW; ++k) t.w[k] = a.block_sum[min(uint64_t(lane) + uint64_t(64 * k), nb - 1)];
     } else {
-        t.w[0] = a.block_base[blk];
+        t.w[0] = kGiven ? given : a.block_base[blk];
     }
     return t;
 }
@@ -467,8 +477,8 @@ __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, 
     }
 }
 
-template <int kU, int kNT, bool kFused, bool kRoot = false>
-__device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile) {
+template <int kU, int kNT, bool kFused, bool kRoot = false, bool kGiven = false>
+__device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile, uint64_t given = 0) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = tile * kEmitRecs;
     uint32_t* img32 = reinterpret_cast<uint32_t*>(T.img);
@@ -478,7 +488,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     // Prologue: the tile-placement loads and this lane's descriptor issued
     // together, one memory round trip before the planning starts.
     ONC_PROF(0);
-    TileLoads<kFused> tl = tile_loads<kFused>(a, tile);
+    TileLoads<kFused> tl = tile_loads<kFused, kGiven>(a, tile, given);
     MsgRegs mr = issue_msg(a.msgs + r0 + min(lane, nrec - 1));
     if constexpr (kFused) {
         static_assert(TileLoads<kFused>::kW == 16, "pin list below");
@@ -898,11 +908,61 @@ __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile
 constexpr int kWsGrid = 1024;   // persistent workgroups (4 per CU on 256 CUs)
 static_assert(kWsGrid / kTilesPerBlk <= 64, "a producer adds at most 64 workgroup totals per tile");
 
+// Header-heavy batches (codec.hip picks this kernel from the declared payload
+// arena, which overstates the payload when it is a decoded wire: a re-encode
+// of configs[0]-shaped records measured enc_emit 99 -> 159 us): every
+// workgroup samples the enc_len totals of the first kWsSample workgroups
+// (enc_len's block_pay: streamed payload bytes) and, when the records
+// average under kWsMinPayload payload bytes, its four waves run the
+// wave-per-tile code instead — each wave its own tiles (g, g + G, ...; G =
+// the grid's waves), placed by a running sum of the enc_len workgroup
+// totals, as the producer does.
+constexpr uint64_t kWsMinPayload = 128;     // bytes per record (the host rule's threshold)
+constexpr uint64_t kWsSample = 64;          // enc_len workgroups sampled (64k records)
+union WsShared {
+    struct {
+        WsSlot slot[2];
+        WsLane ln[64];
+    } ws;
+    ImgTile wpt[4];
+};
+
+__device__ __forceinline__ bool ws_header_heavy(const EncArgs& a) {
+    if (!a.block_pay || (a.variant & 0x10000)) return false;     // 0x10000: the pipeline on every shape (tests)
+    const int lane = threadIdx.x & 63;
+    const uint64_t nb = num_len_blocks(a.n);
+    const uint64_t pay = uint64_t(lane) < min(nb, kWsSample) ? a.block_pay[lane] : 0;
+    const uint64_t recs = min(a.n, kWsSample * kLenRecs);
+    return lane_u64(wave_incl_scan_u64(pay), 63) < kWsMinPayload * recs;
+}
+
+template <int kU, int kNT>
+__device__ __forceinline__ void ws_as_wave_per_tile(const EncArgs& a, ImgTile& T) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t ntiles = num_emit_tiles(a.n), nb = num_len_blocks(a.n);
+    const uint64_t G = uint64_t(gridDim.x) * 4;
+    uint64_t run_blk = 0, run_base = 0;
+    for (uint64_t tile = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); tile < ntiles; tile += G) {
+        // workgroup totals [run_blk, blk): G tiles apart = G / 16 workgroups per step
+        const uint64_t blk = tile / kTilesPerBlk;
+        uint64_t v = 0;
+        for (uint64_t b = run_blk + lane; b < blk; b += 64) v += a.block_sum[min(b, nb - 1)];
+        run_base += lane_u64(wave_incl_scan_u64(v), 63);
+        run_blk = blk;
+        enc_emit_tile<kU, kNT, false, false, true>(a, T, tile, run_base);
+    }
+}
+
 template <int kU, int kNT>
 __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
-    __shared__ WsSlot s_slot[2];
-    __shared__ WsLane s_ln[64];
+    __shared__ WsShared s_sh;
+    WsSlot* s_slot = s_sh.ws.slot;
+    WsLane* s_ln = s_sh.ws.ln;
     const int wv = threadIdx.x >> 6;
+    if (ws_header_heavy(a)) {                       // wave-uniform and grid-uniform
+        ws_as_wave_per_tile<1, kNT>(a, s_sh.wpt[wv]);
+        return;
+    }
     const uint64_t ntiles = num_emit_tiles(a.n);
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.msgs);
     WsTile S;

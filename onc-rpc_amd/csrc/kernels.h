@@ -50,6 +50,8 @@ struct EncArgs {
     uint64_t* tile_sum;     // tiles
     uint64_t* block_sum;    // enc_len workgroups (kLenRecs records): byte totals
     uint64_t* block_base;   // exclusive scan of block_sum (unused when fused_base)
+    uint64_t* block_pay;    // optional: enc_len workgroups' streamed payload bytes (the wave-specialised
+                            // enc_emit's header-heavy test); NULL = not computed
     uint32_t fused_base;    // enc_emit sums block_sum itself (<= kFusedBlocks workgroups; no scan launch)
     uint32_t variant;       // ONC_RPC_VARIANT bits (A/B experiments)
     uint32_t ws;            // enc_emit: the wave-specialised kernel (codec.hip enc_args decides)

@@ -16,7 +16,11 @@ import onc_rpc_amd.synth as S  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
-PATHS = {"ws": "0x200", "tile": "0x400"}
+# ws: the wave-specialised kernel, which runs header-heavy batches as
+# wave-per-tile workers (encode.hip ws_header_heavy); ws_pipeline: the same
+# kernel with that fallback off (0x10000), its producer/consumer pipeline
+# on every shape; tile: the wave-per-tile kernel
+PATHS = {"ws": "0x200", "ws_pipeline": "0x10200", "tile": "0x400"}
 
 
 @pytest.fixture(scope="module")
