@@ -329,7 +329,7 @@ namespace {
 
 // Encoder arguments common to the plan and emit phases.
 int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* rec_len, onc::EncArgs& a,
-             uint32_t root = ONC_ROOT_RPC_MESSAGE) {
+             uint32_t root = ONC_ROOT_RPC_MESSAGE, uint64_t n_whole = 0) {
     const uint64_t tiles = onc::num_emit_tiles(batch->n);
     const int rc = ensure_scratch(c, tiles);
     if (rc != ONC_RC_OK) return rc;
@@ -358,10 +358,13 @@ int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
     // 945 us). Variant bits force it (0x200) or the wave-per-tile kernel
     // (0x400). It places tiles from the workgroup totals itself at any size.
     const uint64_t n = batch->n;
+    // the arena's bytes per record are those of the whole batch (a chunk of
+    // a chunked encode shares its arenas)
+    const uint64_t nw = n_whole ? n_whole : n;
     // a.ws: 0 wave-per-tile; 1 wave-specialised, 2 KiB consumer steps; 2 the
     // same with 1 KiB steps (long payloads: configs[3] 1770 vs 1815 us)
-    const bool big = batch->payload_len >= 512 * n;
-    const bool ws_shape = batch->payload_len >= 128 * n && (onc::num_emit_tiles(n) <= kWsMaxTiles || big);
+    const bool big = batch->payload_len >= 512 * nw;
+    const bool ws_shape = batch->payload_len >= 128 * nw && (onc::num_emit_tiles(n) <= kWsMaxTiles || big);
     a.ws = ((c->variant & 0x200) || (!(c->variant & 0x400) && n && ws_shape)) ? (big ? 2u : 1u) : 0u;
     a.root = root;
     if (root != ONC_ROOT_RPC_MESSAGE) a.ws = 0;   // body roots: the wave-per-tile kernel
@@ -375,9 +378,9 @@ int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
 
 // enc_len: plans + per-tile and per-workgroup byte totals into the scratch.
 int enc_plan(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* rec_len,
-             uint32_t root = ONC_ROOT_RPC_MESSAGE) {
+             uint32_t root = ONC_ROOT_RPC_MESSAGE, uint64_t n_whole = 0) {
     onc::EncArgs a;
-    int rc = enc_args(c, batch, status, rec_len, a, root);
+    int rc = enc_args(c, batch, status, rec_len, a, root, n_whole);
     if (rc != ONC_RC_OK) return rc;
     forget_plan(c);
     rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
@@ -393,9 +396,10 @@ int enc_plan(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
 // [scan of the workgroup totals, with the grand total into rec_off[n]] +
 // enc_emit: the bytes, placed by the plan in the scratch.
 int enc_emit(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
-             int32_t* status, uint32_t* rec_len, uint32_t root = ONC_ROOT_RPC_MESSAGE) {
+             int32_t* status, uint32_t* rec_len, uint32_t root = ONC_ROOT_RPC_MESSAGE, uint64_t n_whole = 0,
+             const uint64_t* base_dev = nullptr) {
     onc::EncArgs a;
-    int rc = enc_args(c, batch, status, rec_len, a, root);
+    int rc = enc_args(c, batch, status, rec_len, a, root, n_whole);
     if (rc != ONC_RC_OK) return rc;
     // any writer position: the kernels work on 16-byte chunks from the
     // aligned address below `out`, whose first `origin` bytes are never written
@@ -404,6 +408,7 @@ int enc_emit(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_ca
     a.out_cap = out ? a.origin + out_cap : 0;
     a.rec_off = rec_off;
     a.rec_len = nullptr;   // written by the plan
+    a.base_dev = base_dev;
     if (!a.fused_base) {
         const uint64_t nblk = onc::num_len_blocks(batch->n);
         rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
@@ -412,6 +417,38 @@ int enc_emit(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_ca
         if (rc != ONC_RC_OK) return rc;
     }
     return run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
+}
+
+// plan + emit of a whole batch. Beyond kEncChunk records the batch is
+// encoded as consecutive chunks of kEncChunk records, each planned right
+// before it is emitted: enc_emit then reads the descriptors enc_len has just
+// read (64 MB per chunk: held by the 256 MB Infinity Cache) instead of
+// descriptors a whole-batch enc_len read hundreds of MB earlier, and every
+// chunk places its tiles by summing its own workgroup totals (no scan
+// launch). Chunk k + 1 starts where chunk k ended: its kernels read that
+// offset from rec_off[k's end], which chunk k's emit wrote.
+constexpr uint64_t kEncChunk = onc::kFusedBlocks * onc::kLenRecs;   // 1M records
+
+int encode_batch(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
+                 int32_t* status, uint32_t* rec_len, uint32_t root) {
+    const uint64_t n = batch->n;
+    if (n <= kEncChunk || (c->variant & 0x40000)) {     // 0x40000: whole-batch plan (lab)
+        const int rc = enc_plan(c, batch, status, rec_len, root);
+        if (rc != ONC_RC_OK) return rc;
+        return enc_emit(c, batch, out, out_cap, rec_off, status, nullptr, root);
+    }
+    for (uint64_t c0 = 0; c0 < n; c0 += kEncChunk) {
+        onc_batch sub = *batch;
+        sub.n = std::min(kEncChunk, n - c0);
+        sub.msgs = batch->msgs + c0;
+        int rc = enc_plan(c, &sub, status + c0, rec_len ? rec_len + c0 : nullptr, root, n);
+        if (rc != ONC_RC_OK) return rc;
+        rc = enc_emit(c, &sub, out, out_cap, rec_off + c0, status + c0, nullptr, root, n,
+                      c0 ? rec_off + c0 : nullptr);
+        if (rc != ONC_RC_OK) return rc;
+    }
+    forget_plan(c);
+    return ONC_RC_OK;
 }
 
 }  // namespace
@@ -425,9 +462,7 @@ int onc_encode(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_
         const hipError_t e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
         return e == hipSuccess ? ONC_RC_OK : fail(c, e, "hipMemsetAsync");
     }
-    const int rc = enc_plan(c, batch, status, rec_len);
-    if (rc != ONC_RC_OK) return rc;
-    return enc_emit(c, batch, out, out_cap, rec_off, status, nullptr);
+    return encode_batch(c, batch, out, out_cap, rec_off, status, rec_len, ONC_ROOT_RPC_MESSAGE);
 }
 
 int onc_encode_plan(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* rec_len) {
@@ -727,9 +762,7 @@ int onc_encode_body(onc_codec* c, int root, const onc_batch* batch, uint8_t* out
         const hipError_t e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
         return e == hipSuccess ? ONC_RC_OK : fail(c, e, "hipMemsetAsync");
     }
-    const int rc = enc_plan(c, batch, status, rec_len, uint32_t(root));
-    if (rc != ONC_RC_OK) return rc;
-    return enc_emit(c, batch, out, out_cap, rec_off, status, nullptr, uint32_t(root));
+    return encode_batch(c, batch, out, out_cap, rec_off, status, rec_len, uint32_t(root));
 }
 
 int32_t onc_expected_message_len(const uint8_t* data, uint64_t len, uint32_t* out) {

@@ -148,6 +148,11 @@ __device__ __forceinline__ uint64_t tile_reduce(const TileLoads<kFused>& t, uint
     return t.w[0] + lane_u64(wave_incl_scan_u64(v), 63);
 }
 
+// Bytes the caller's earlier launches already placed before this launch's
+// first record (onc_encode of a batch in chunks: the previous chunk's end,
+// read from the rec_off it wrote); 0 for a whole batch.
+__device__ __forceinline__ uint64_t launch_base(const EncArgs& a) { return a.base_dev ? *a.base_dev : 0ull; }
+
 constexpr int kFastWaves = 4;                 // wave tiles per enc_emit workgroup
 
 // Phase timestamps of a tile (lab builds with -DONC_EMIT_PROF only):
@@ -502,7 +507,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     const onc_msg dm = as_msg(mr);
     // output coordinates: byte 0 = the 16-aligned chunk base below the
     // caller's `out`, which sits at `origin` (any writer position)
-    const uint64_t T0 = a.origin + tile_reduce<kFused>(tl, tile);
+    const uint64_t T0 = a.origin + (kGiven ? 0ull : launch_base(a)) + tile_reduce<kFused>(tl, tile);
     ONC_PROF(1);
     uint64_t len = 0, poff = 0;
     uint32_t hw = 0;
@@ -941,7 +946,7 @@ __device__ __forceinline__ void ws_as_wave_per_tile(const EncArgs& a, ImgTile& T
     const int lane = threadIdx.x & 63;
     const uint64_t ntiles = num_emit_tiles(a.n), nb = num_len_blocks(a.n);
     const uint64_t G = uint64_t(gridDim.x) * 4;
-    uint64_t run_blk = 0, run_base = 0;
+    uint64_t run_blk = 0, run_base = launch_base(a);
     for (uint64_t tile = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); tile < ntiles; tile += G) {
         // workgroup totals [run_blk, blk): G tiles apart = G / 16 workgroups per step
         const uint64_t blk = tile / kTilesPerBlk;
@@ -967,7 +972,7 @@ __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.msgs);
     WsTile S;
     S.run_blk = 0;
-    S.run_base = 0;
+    S.run_base = launch_base(a);
     uint64_t next = blockIdx.x;
     bool have = false;
     // producer: one span into slot W, or "done"

@@ -56,6 +56,7 @@ struct EncArgs {
     uint32_t variant;       // ONC_RPC_VARIANT bits (A/B experiments)
     uint32_t ws;            // enc_emit: the wave-specialised kernel (codec.hip enc_args decides)
     uint32_t root;          // ONC_ROOT_* (onc_encode_body); ONC_ROOT_RPC_MESSAGE for onc_encode
+    const uint64_t* base_dev;   // optional: output bytes before this launch's first record (chunked encode)
 #ifdef ONC_EMIT_PROF
     uint64_t* prof;         // lab builds only (tools/emit_prof.hip): per-tile phase timestamps
 #endif

@@ -10,4 +10,5 @@ for f in sys.argv[1:]:
         continue
     k = d["kernels_breakdown_pass"]
     print(f, round(d["value"], 1), round(d["ms_per_step"] * 1e3, 1), "us/step",
-          {n: round(v["avg_us"], 1) for n, v in k.items()}, "frac", round(d["roofline"]["frac"], 3))
+          {n: round(v["avg_us"] * v.get("launches_per_step", 1), 1) for n, v in k.items()}, "us/step per kernel;",
+          "frac", round(d["roofline"]["frac"], 3), d["roofline"]["kernel"])

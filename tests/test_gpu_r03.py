@@ -179,3 +179,32 @@ def test_bench_two_ranks_line_has_cpu_baseline():
     cb = r["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["sample_bit_exact_vs_gpu"] is True
     assert "after all 2 ranks" in cb["note"]
+
+
+@pytest.mark.parametrize("shift,cap_frac", [(0, None), (7, None), (3, 0.6)])
+def test_chunked_encode_bit_exact(codec, R, oracle, shift, cap_frac):
+    """onc_encode beyond 1M records runs as 1M-record chunks, each planned
+    right before it is emitted (codec.hip encode_batch): records across the
+    chunk boundary at any writer position (byte path: odd payloads), with the
+    capacity ending inside the second chunk — bytes, offsets and statuses
+    equal to the oracle's whole-batch loop."""
+    import torch
+    hb = S.mixed(1_100_000, seed=5, pmin=0, pmax=300, exotic=0.1)
+    o_wire, o_off, o_st, o_len = oracle.encode_batch(hb)
+    total = len(o_wire)
+    cap = total if cap_frac is None else int(total * cap_frac)
+    if cap != total:
+        o_wire, o_off, o_st, o_len = oracle.encode_batch(hb, out_cap=cap)
+    db = R.DeviceBatch.from_host(hb)
+    buf = torch.full((shift + total + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    off = torch.empty(hb.n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(hb.n, dtype=torch.int32, device="cuda")
+    rl = torch.empty(hb.n, dtype=torch.int32, device="cuda")
+    codec.encode(db, buf[shift:], off, st, rl, out_cap=cap)
+    codec.sync()
+    b = buf.cpu().numpy()
+    assert np.array_equal(st.cpu().numpy(), o_st)
+    assert np.array_equal(off.cpu().numpy().view(np.uint64), o_off)
+    assert np.array_equal(rl.cpu().numpy().view(np.uint32), o_len)
+    assert b[shift:shift + len(o_wire)].tobytes() == o_wire
+    assert (b[:shift] == 0xA5).all() and (b[shift + cap:] == 0xA5).all()
