@@ -23,6 +23,7 @@ struct onc_codec {
     uint8_t* frame_scratch = nullptr;   // onc_frame_stream per-chunk state
     uint64_t frame_chunks = 0;
     uint64_t frame_chunk = onc::kFrameChunkDefault;   // ONC_RPC_FRAME_CHUNK at create (bytes, >= 64)
+    uint64_t enc_chunk = 0;    // ONC_RPC_ENC_CHUNK at create (records, multiple of 1024; 0 = kEncChunk)
     bool force_scan = false;   // ONC_RPC_FORCE_SCAN=1 at create: always launch the block scan (tests)
     uint32_t variant = 0;      // ONC_RPC_VARIANT at create: kernel variant bits (A/B measurements)
     // the batch whose plan (onc_encode_plan) the scratch holds, and the
@@ -157,6 +158,8 @@ int onc_codec_create(onc_codec** out, int device, void* hip_stream) {
     c->force_scan = fs && fs[0] == '1';
     const char* vv = getenv("ONC_RPC_VARIANT");
     if (vv) c->variant = uint32_t(strtoul(vv, nullptr, 0));
+    const char* ec = getenv("ONC_RPC_ENC_CHUNK");
+    if (ec) c->enc_chunk = strtoull(ec, nullptr, 10) / onc::kLenRecs * onc::kLenRecs;
     const char* fc = getenv("ONC_RPC_FRAME_CHUNK");
     if (fc) {
         const unsigned long long v = strtoull(fc, nullptr, 10);
@@ -432,14 +435,15 @@ constexpr uint64_t kEncChunk = onc::kFusedBlocks * onc::kLenRecs;   // 1M record
 int encode_batch(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
                  int32_t* status, uint32_t* rec_len, uint32_t root) {
     const uint64_t n = batch->n;
-    if (n <= kEncChunk || (c->variant & 0x40000)) {     // 0x40000: whole-batch plan (lab)
+    const uint64_t chunk = c->enc_chunk ? c->enc_chunk : kEncChunk;
+    if (n <= chunk || (c->variant & 0x40000)) {     // 0x40000: whole-batch plan (lab)
         const int rc = enc_plan(c, batch, status, rec_len, root);
         if (rc != ONC_RC_OK) return rc;
         return enc_emit(c, batch, out, out_cap, rec_off, status, nullptr, root);
     }
-    for (uint64_t c0 = 0; c0 < n; c0 += kEncChunk) {
+    for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
         onc_batch sub = *batch;
-        sub.n = std::min(kEncChunk, n - c0);
+        sub.n = std::min(chunk, n - c0);
         sub.msgs = batch->msgs + c0;
         int rc = enc_plan(c, &sub, status + c0, rec_len ? rec_len + c0 : nullptr, root, n);
         if (rc != ONC_RC_OK) return rc;
