@@ -562,17 +562,33 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
         const uint64_t wg = blockIdx.x;
         const uint64_t blk = wg / (kDecLenBlk / kDecTile);
         const uint64_t w0 = blk * (kDecLenBlk / kDecTile);
-        const uint32_t len = valid ? a.rec_len[i] : 0u;
-        const uint64_t ts = w0 + t < wg ? a.tile_sum[w0 + t] : 0;
+        // every prologue load issued unconditionally (clamped indices) and
+        // pinned, then masked: one memory round trip (loads under
+        // per-lane branches made the compiler wait for the length before
+        // issuing the totals: two)
+        const uint64_t nwg = (a.n + kDecTile - 1) / kDecTile;
+        const auto clamp = [](uint64_t x, uint64_t hi) { return x < hi ? x : hi; };
+        uint32_t len = a.rec_len[clamp(i, a.n - 1)];
+        uint64_t ts = a.tile_sum[clamp(w0 + t, nwg - 1)];
+        constexpr int kPre = kBlkFused ? int(kDecLenFusedBlocks / 64) : 1;
+        uint64_t pv[kPre];
+#pragma unroll
+        for (int k = 0; k < kPre; ++k)
+            pv[k] = kBlkFused ? a.blk_sum[clamp(uint64_t(t) + 64ull * k, a.nblk - 1)] : a.blk_base[blk];
+        static_assert(kPre == 1 || kPre == 8, "pin list below");
+        if constexpr (kPre == 8)
+            asm volatile("" : "+v"(len), "+v"(ts), "+v"(pv[0]), "+v"(pv[1]), "+v"(pv[2]), "+v"(pv[3]), "+v"(pv[4]),
+                         "+v"(pv[5]), "+v"(pv[6]), "+v"(pv[7]));
+        else
+            asm volatile("" : "+v"(len), "+v"(ts), "+v"(pv[0]));
+        len = valid ? len : 0u;
+        ts = w0 + t < wg ? ts : 0;
         uint64_t pre = 0;
         if constexpr (kBlkFused) {
 #pragma unroll
-            for (int k = 0; k < int(kDecLenFusedBlocks / 64); ++k) {
-                const uint64_t j = uint64_t(t) + 64ull * k;
-                pre += j < blk ? a.blk_sum[j] : 0;
-            }
+            for (int k = 0; k < kPre; ++k) pre += uint64_t(t) + 64ull * k < blk ? pv[k] : 0;
         } else {
-            pre = t == 0 ? a.blk_base[blk] : 0;
+            pre = t == 0 ? pv[0] : 0;
         }
         const uint64_t incl = wave_incl_scan_u64(uint64_t(len));
         const uint64_t wbase = a.base + lane_u64(wave_incl_scan_u64(pre + ts), 63);
@@ -598,10 +614,15 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
         const uint32_t avail = uint32_t(min(uint64_t(kWinChunks), (q0 + L + 15) >> 4));
         const uint32_t r1 = kExact && !kRoot ? uint32_t(min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4)) : kWin1;
         nch = min(r1, avail);
+        // all kWin1 loads issued without a per-chunk branch (chunks past the
+        // record's last granule re-read that granule) and pinned: under
+        // branches the compiler waited for chunk 2 before issuing chunk 3
         u32x4 v[kWin1];
+        const uintptr_t last = win + 16 * (nch - 1);          // nch >= 1 here (L != 0)
 #pragma unroll
-        for (uint32_t j = 0; j < kWin1; ++j)
-            if (j < nch) v[j] = gload<u32x4>(win + 16 * j);
+        for (uint32_t j = 0; j < kWin1; ++j) v[j] = gload<u32x4>(min(win + 16 * j, last));
+        static_assert(kWin1 == 4, "pin list below");
+        asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
         // stored shifted by d0 dwords: column word 0 holds record byte 0's dword
 #pragma unroll
         for (uint32_t j = 0; j < kWin1; ++j) {
