@@ -46,8 +46,10 @@ extern "C" {
  *    now runs inside frame_chunks; ONC_K_FRAME_VERIFY is gone).
  * 4: body-level roots (ONC_ROOT_*, onc_decode_body, onc_encode_body,
  *    onc_encode_body_lengths); timing id 10 retired (ONC_K_FRAME_OFFSETS
- *    gone, the framer ids after it move down by one). */
-#define ONC_RPC_ABI_VERSION 4
+ *    gone, the framer ids after it move down by one).
+ * 5: decoded AUTH_UNIX slots compacted per 64-record group (onc_decoded):
+ *    a slot's index is only what onc_auth.ref says, no longer 2i / 2i + 1. */
+#define ONC_RPC_ABI_VERSION 5
 
 /* ------------------------------------------------------------------------ */
 /* Wire discriminants (values are the on-wire u32s)                          */
@@ -129,8 +131,8 @@ extern "C" {
  *                   payload (no verifier)
  *  REJECTED_REPLY   msg_type REPLY, reply_stat DENIED, stat, u.mismatch / auth_stat
  *  AUTH_ERROR       msg_type REPLY, reply_stat DENIED, stat AUTH_ERROR, auth_stat
- *  AUTH_FLAVOR      msg_type CALL, the value in cred (AUTH_UNIX: decode slot 2i)
- *  AUTH_UNIX_PARAMS msg_type CALL, cred kind UNIX (decode: slot 2i)
+ *  AUTH_FLAVOR      msg_type CALL, the value in cred (AUTH_UNIX: slot cred.ref)
+ *  AUTH_UNIX_PARAMS msg_type CALL, cred kind UNIX (slot cred.ref)
  *  OPAQUE           msg_type CALL, cred kind NONE, its body = the opaque's
  * A descriptor of another shape encodes as ONC_ENC_BAD_DESCRIPTOR. */
 #define ONC_ROOT_RPC_MESSAGE      0
@@ -279,14 +281,18 @@ typedef struct onc_batch {
 } onc_batch;
 
 /* Decode outputs. [dev] pointers.
- * unix_params has 2*n slots: record i's credentials use slot 2i, its
- * verifier slot 2i+1 (the slot index is stored in onc_auth.ref).
+ * unix_params has 2*n slots. The AUTH_UNIX parameter sets of the OK records
+ * of each 64-record group [64g, 64g + 64) (counted from the call's first
+ * record) take consecutive slots from 128g, in record order, credential
+ * before verifier; onc_auth.ref holds the slot index. Slots past a group's
+ * last set are not written. (Packed, the sets of a group are written as
+ * whole contiguous lines: a slot pair per record, 2i / 2i + 1, scattered
+ * them 192 bytes apart.)
  * Offsets in the decoded descriptors are wire-buffer offsets, so a decoded
- * batch can be re-encoded with auth_arena = payload_arena = wire.
- * For a record with status != ONC_OK the descriptor is all zero; unix slots
- * are defined only for OK records whose auth kind is UNIX (the decoder may
- * zero the other bytes of a record's 192-byte slot pair, to write whole
- * 64-byte sectors). */
+ * batch can be re-encoded with auth_arena = payload_arena = wire and
+ * unix_params as the AUTH_UNIX table (unix_count = 2n).
+ * For a record with status != ONC_OK the descriptor is all zero and it takes
+ * no slot. */
 typedef struct onc_decoded {
     onc_msg*         msgs;        /* n */
     onc_unix_params* unix_params; /* 2n */

@@ -37,45 +37,34 @@ constexpr uint32_t kWinWords = 4 * kWinChunks;
 #define ONC_DEC_TILE 64     // c1 decode 54.7 -> 50.2 us, c2 81 -> 78.6, c3 447 -> 468 vs 256 (profiles/lab_r02_dec_tile.log)
 #endif
 constexpr int kDecTile = ONC_DEC_TILE;
-#ifndef ONC_DEC_STAGE_MIN
-#define ONC_DEC_STAGE_MIN 32   // AUTH_UNIX records in a workgroup from which its slots are staged
-#endif        // records (lanes) per decode workgroup
+constexpr uint32_t kSlotPass = 96;       // AUTH_UNIX slots staged per pass (9 KiB of the window)
 
-// The window column holds the record's words dword-aligned to the record:
-// column word k = record bytes [4k - sh, 4k - sh + 4) (the loaded 16-byte
-// granules stored shifted by the record's dword offset in its first
-// granule), so record word k is column word k when the record starts on a
-// 4-byte boundary and a funnel of words k and k + 1 otherwise — fields at
-// fixed record positions read at fixed LDS offsets.
+// The window column holds the record's words aligned to the record: column
+// word k = record bytes [4k, 4k + 4), whatever the record's byte offset in
+// its first 16-byte granule (the loaded granules are stored shifted by that
+// offset, each column word funnelled from two loaded words once, at staging)
+// — every field read is one LDS read at a fixed offset. (Funnelling at each
+// read instead cost the configs[2] decode 70 -> 55 us against a lab build
+// that assumed aligned records.)
 struct Rd {
     uintptr_t base;          // absolute address of record byte 0
-    uint32_t sh;             // record byte 0's offset in its dword (0..3)
     uint32_t lim;            // record bytes held by the window
     const uint32_t* col;     // this lane's window column (stride kDecTile words)
 
     // Big-endian u32 at record-relative position pos (pos % 4 == 0; all 4 bytes valid).
     __device__ __forceinline__ uint32_t be32(uint32_t pos) const {
-        if (pos + 4u <= lim) {
-            const uint32_t k = pos >> 2;
-            const uint32_t w0 = col[k * kDecTile];
-            const uint32_t w1 = sh ? col[(k + 1) * kDecTile] : 0u;
-            return bswap(funnel(w0, w1, sh));
-        }
+        if (pos + 4u <= lim) return bswap(col[(pos >> 2) * kDecTile]);
         return bswap(load4(base + pos));
     }
 
     // n (<= 16) consecutive words from record position pos into out[0..n),
-    // zeros after: straight from the window (17 LDS reads at fixed offsets,
-    // each word's bytes funnelled from two neighbours) when all of them lie
-    // in it, else word by word.
+    // zeros after: straight from the window (16 LDS reads at fixed offsets)
+    // when all of them lie in it, else word by word.
     __device__ __forceinline__ void words16(uint32_t pos, uint32_t n, uint32_t out[ONC_MAX_GIDS]) const {
         if (pos + 4u * n <= lim) {
             const uint32_t* p = col + (pos >> 2) * kDecTile;
-            uint32_t w[ONC_MAX_GIDS + 1];
 #pragma unroll
-            for (uint32_t k = 0; k <= ONC_MAX_GIDS; ++k) w[k] = (k < n || (k == n && sh)) ? p[k * kDecTile] : 0u;
-#pragma unroll
-            for (uint32_t g = 0; g < ONC_MAX_GIDS; ++g) out[g] = g < n ? bswap(funnel(w[g], w[g + 1], sh)) : 0u;
+            for (uint32_t g = 0; g < ONC_MAX_GIDS; ++g) out[g] = g < n ? bswap(p[g * kDecTile]) : 0u;
         } else {
 #pragma unroll
             for (uint32_t g = 0; g < ONC_MAX_GIDS; ++g) out[g] = g < n ? be32(pos + 4u * g) : 0u;
@@ -97,29 +86,15 @@ struct Rules {
     static constexpr int32_t kShort = MODE == ONC_DECODE_BYTES ? ONC_ERR_INVALID_LENGTH : ONC_ERR_IO_UNEXPECTED_EOF;
 };
 
-// One decoded AUTH_UNIX parameter slot, written with six dwordx4 stores.
-// A record's two slots are 192 bytes = three 64-byte sectors; one slot alone
-// would leave the middle sector half written (a read-modify-write in the
-// memory controller), so the slot is padded to whole sectors with 32 zero
-// bytes of the record's other slot, which is unspecified unless it holds an
-// AUTH_UNIX verifier (written after the credential, so it wins).
-//   pad: 1 = credential slot (zeros after it), 2 = verifier slot whose
-//   credential slot is unused (zeros before it), 0 = no padding.
-// Output stores: the decoded descriptors (staged through LDS, 16 KiB
-// contiguous per workgroup) and the status / aux arrays fill whole lines
-// and are stored nontemporally — the decoder never reads them back, and
-// plain stores leave dirty lines for the next kernel to write back
-// (measured: c1 step +2-3 %, c3 +2 %; tools/store_lab.hip for the
-// mechanism). AUTH_UNIX slots are written lane by lane (192 bytes at a
-// 192-byte stride) and keep plain stores: L2 merges the neighbouring
-// lanes' pieces into whole lines, where nontemporal stores send each piece
-// to memory as a partial line (c3 decode 450 -> 1040-1300 us); for sparse
-// slots (configs[2]: a quarter of the records) the two policies measured
-// within the run-to-run spread.
-// AUTH_UNIX parameters of a record's credential (slot 2i, k = 0) and
-// verifier (slot 2i + 1, k = 1), held in registers until the record is
-// parsed, then written out (see the end of decode_kernel): 24 words per
-// slot in onc_unix_params order.
+// Output stores: the decoded descriptors (staged through LDS, 4 KiB
+// contiguous per workgroup), the AUTH_UNIX slots (compacted per workgroup,
+// staged) and the status / aux arrays fill whole lines and are stored
+// nontemporally — the decoder never reads them back, and plain stores leave
+// dirty lines for the next kernel to write back (measured: c1 step +2-3 %,
+// c3 +2 %; tools/store_lab.hip for the mechanism).
+// AUTH_UNIX parameters of a record's credential (k = 0) and verifier
+// (k = 1), held in registers until the record is parsed, then written out
+// (see the end of decode_kernel): 24 words per slot in onc_unix_params order.
 struct UnixSlots {
     uint32_t w[2][24];
     uint32_t mask;      // bit k: slot k holds parameters
@@ -138,32 +113,6 @@ __device__ __forceinline__ void put_unix(UnixSlots& us, uint64_t slot, uint32_t 
 #pragma unroll
     for (int g = 0; g < 16; ++g) us.w[k][8 + g] = gids[g];
     us.mask |= 1u << k;
-}
-
-// One lane's slots straight to global memory (waves with few AUTH_UNIX
-// records), padded to whole 64-byte sectors: the credential slot with the
-// verifier slot's first 32 bytes zeroed (when that slot has no parameters),
-// the verifier slot with the credential slot's last 32 bytes zeroed (when
-// that one has none) — partial 64-byte sectors cost a read-modify-write
-// (c3 decode 537 -> 454 us with the padding).
-__device__ __forceinline__ void put_unix_direct(onc_unix_params* pair, const UnixSlots& us) {
-    uint4* d = reinterpret_cast<uint4*>(pair);          // 12 x 16 bytes: [cred 0..5][verf 6..11]
-    if (us.mask & 1u) {
-#pragma unroll
-        for (int q = 0; q < 6; ++q) d[q] = make_uint4(us.w[0][4 * q], us.w[0][4 * q + 1], us.w[0][4 * q + 2], us.w[0][4 * q + 3]);
-        if (!(us.mask & 2u)) {
-            d[6] = make_uint4(0, 0, 0, 0);
-            d[7] = make_uint4(0, 0, 0, 0);
-        }
-    }
-    if (us.mask & 2u) {
-        if (!(us.mask & 1u)) {
-            d[4] = make_uint4(0, 0, 0, 0);
-            d[5] = make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < 6; ++q) d[6 + q] = make_uint4(us.w[1][4 * q], us.w[1][4 * q + 1], us.w[1][4 * q + 2], us.w[1][4 * q + 3]);
-    }
 }
 
 // Slice mode AuthFlavor::from_cursor (flavor.rs:52-94) with
@@ -623,21 +572,28 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
         for (uint32_t j = 0; j < kWin1; ++j) v[j] = gload<u32x4>(min(win + 16 * j, last));
         static_assert(kWin1 == 4, "pin list below");
         asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
-        // stored shifted by d0 dwords: column word 0 holds record byte 0's dword
+        // column word c = record bytes [4c, 4c + 4): loaded words d0 + c and
+        // d0 + c + 1 funnelled by the record's byte offset in its dword. The
+        // last word of the round (its upper bytes in the next chunk) is
+        // rewritten if round 2 loads that chunk; otherwise it lies past `lim`.
+        const uint32_t sh = q0 & 3u;
+        uint32_t e[4 * kWin1 + 1];
 #pragma unroll
         for (uint32_t j = 0; j < kWin1; ++j) {
-            if (j < nch) {
-                const uint32_t e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-#pragma unroll
-                for (uint32_t k = 0; k < 4; ++k)
-                    if (4 * j + k >= d0) s_win[(4 * j + k - d0) * kDecTile + t] = e[k];
-            }
+            e[4 * j] = v[j].x;
+            e[4 * j + 1] = v[j].y;
+            e[4 * j + 2] = v[j].z;
+            e[4 * j + 3] = v[j].w;
         }
+        e[4 * kWin1] = 0u;
+#pragma unroll
+        for (uint32_t r = 0; r < 4 * kWin1; ++r)
+            if (r >= d0 && r < 4 * nch) s_win[(r - d0) * kDecTile + t] = funnel(e[r], e[r + 1], sh);
         // Header extent from the first round: call -> 36 + cred body + verf
         // flavor/length + the verifier body (its length when the first round
         // holds it, else a 16-byte guess); reply -> up to 12 bytes past an
         // accepted verifier.
-        const Rd R1{base, q0 & 3u, 16 * nch - q0, &s_win[t]};
+        const Rd R1{base, 16 * nch - q0, &s_win[t]};
         uint32_t need = uint32_t(min(L, uint64_t(16 * kWinChunks)));
         if (!kRoot && L >= 36 && 16 * nch >= q0 + 36) {
             const uint32_t mt = R1.be32(8);
@@ -662,22 +618,40 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
             // chunks [nch, want): from kR2 on (the first chunk round 1 may
             // have skipped) up to the window's end
             constexpr uint32_t kR2 = kExact && !kRoot ? 3u : kWin1;   // round 1 held >= 3 chunks if L >= 44
-            u32x4 w[kWinChunks > kR2 ? kWinChunks - kR2 : 1];
+            constexpr uint32_t kN2 = kWinChunks > kR2 ? kWinChunks - kR2 : 1;
+            u32x4 w[kN2];
+#pragma unroll
+            for (uint32_t j = 0; j < kN2; ++j) w[j] = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
             for (uint32_t j = kR2; j < kWinChunks; ++j)
                 if (j >= nch && j < want) w[j - kR2] = gload<u32x4>(win + 16 * j);
+            uint32_t f[4 * kN2 + 1];
 #pragma unroll
-            for (uint32_t j = kR2; j < kWinChunks; ++j) {
-                if (j >= nch && j < want) {
-                    const uint32_t e[4] = {w[j - kR2].x, w[j - kR2].y, w[j - kR2].z, w[j - kR2].w};
-#pragma unroll
-                    for (uint32_t k = 0; k < 4; ++k) s_win[(4 * j + k - d0) * kDecTile + t] = e[k];   // j >= 3 > d0
-                }
+            for (uint32_t j = 0; j < kN2; ++j) {
+                f[4 * j] = w[j].x;
+                f[4 * j + 1] = w[j].y;
+                f[4 * j + 2] = w[j].z;
+                f[4 * j + 3] = w[j].w;
             }
+            f[4 * kN2] = 0u;
+#pragma unroll
+            for (uint32_t r = 4 * kR2; r < 4 * kWinChunks; ++r)       // r >= 12 > d0
+                if (r >= 4 * nch && r < 4 * want) s_win[(r - d0) * kDecTile + t] = funnel(f[r - 4 * kR2], f[r - 4 * kR2 + 1], sh);
+            // round 1's last word, now with its upper bytes (nch >= kR2 here)
+            uint32_t lo = e[4 * kWin1 - 1], hi = w[0].x;
+#pragma unroll
+            for (uint32_t c = kR2; c < kWin1; ++c)
+                if (nch == c) {
+                    lo = e[4 * c - 1];
+                    hi = w[c - kR2].x;
+                }
+            if (nch == kWin1 && kWin1 - kR2 < kN2) hi = w[kWin1 - kR2].x;
+            s_win[(4 * nch - 1 - d0) * kDecTile + t] = funnel(lo, hi, sh);
             nch = want;
         }
     }
-    const Rd R{base, q0 & 3u, nch ? 16 * nch - q0 : 0u, &s_win[t]};
+    const uint32_t lim = nch ? 16 * nch - q0 : 0u;
+    const Rd R{base, lim, &s_win[t]};
     onc_msg m;
     uint4* mz = reinterpret_cast<uint4*>(&m);
 #pragma unroll
@@ -717,56 +691,49 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
             a.out.aux1[i] = aux1;
         }
     }
+    // AUTH_UNIX slots, compacted per 64-record group: the group's OK records'
+    // parameter sets take consecutive slots from 2 * i0 (record order,
+    // credential before verifier; onc_auth.ref names the slot), staged in the
+    // window and written as whole contiguous lines with nontemporal stores.
+    // Scattered slots (slot 2i / 2i + 1, lane by lane, 192 bytes apart) cost
+    // the configs[2] decode ~20 of its 70 us for 24 % AUTH_UNIX records
+    // (lab build without slot stores: 50.5 us; tools/line_lab.hip: 128 B at
+    // 192 * i 21 us, compacted per lane 13 us).
+    const bool okr = valid && st == ONC_OK;
+    const uint64_t bc = __ballot(okr && (us.mask & 1u)), bv = __ballot(okr && (us.mask & 2u));
+    const uint32_t nslots = uint32_t(__popcll(bc) + __popcll(bv));
     __syncthreads();                                  // every lane is done with its window
-    // AUTH_UNIX slots. When at least half the workgroup's records carry
-    // parameters, the slot pairs of 32 records at a time (6 KiB, contiguous
-    // in the output) are staged in the window and written with coalesced
-    // nontemporal stores, skipping the 64-byte sectors of slots without
-    // parameters: per-lane 16-byte stores 192 bytes apart touch 64 lines per
-    // instruction (configs[3] decode 473 us with them, 411 us staged with
-    // every sector, 275 us with no slot stores at all). Otherwise each lane
-    // writes its own.
-    const uint64_t um = __ballot(us.mask != 0);
-    if (um) {
-        static_assert(kDecTile == 64, "slot staging: one wave, two halves of 32 records");
-        if (__popcll(um) >= ONC_DEC_STAGE_MIN) {
-            uint4* stg = reinterpret_cast<uint4*>(s_win);
+    if (nslots) {
+        const uint64_t below = (1ull << t) - 1;
+        const uint32_t rank = uint32_t(__popcll(bc & below) + __popcll(bv & below));
+        const uint64_t sbase = 2 * i0;
+        if (okr && (us.mask & 1u)) m.cred.ref = sbase + rank;
+        if (okr && (us.mask & 2u)) m.verf.ref = sbase + rank + (us.mask & 1u);
+        static_assert(kWinWords * kDecTile * 4 >= kSlotPass * sizeof(onc_unix_params), "slot staging fits the window");
+        uint4* stg = reinterpret_cast<uint4*>(s_win);
+        u32x4* dst = reinterpret_cast<u32x4*>(a.out.unix_params + sbase);
+        for (uint32_t p0 = 0; p0 < nslots; p0 += kSlotPass) {
+            if (p0) __syncthreads();                  // the previous pass's stores have read the window
+            if (okr) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (h) __syncthreads();                   // the first half's stores have read the window
-                if ((t >> 5) == h) {
-                    uint4* d = stg + 12 * (t & 31);
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        const bool on = (us.mask >> k) & 1u;
+                for (uint32_t k = 0; k < 2; ++k) {
+                    const uint32_t r = rank + (k ? (us.mask & 1u) : 0u) - p0;
+                    if (((us.mask >> k) & 1u) && r < kSlotPass) {
+                        uint4* d = stg + 6 * r;
 #pragma unroll
                         for (int q = 0; q < 6; ++q)
-                            d[6 * k + q] = on ? make_uint4(us.w[k][4 * q], us.w[k][4 * q + 1], us.w[k][4 * q + 2],
-                                                           us.w[k][4 * q + 3])
-                                              : make_uint4(0, 0, 0, 0);
-                    }
-                }
-                __syncthreads();
-                const uint64_t r0 = i0 + 32ull * h;
-                uint4* dst = reinterpret_cast<uint4*>(a.out.unix_params + 2 * r0);
-#pragma unroll
-                for (int c = 0; c < 6; ++c) {
-                    const uint32_t q = uint32_t(t + 64 * c);      // 16-byte chunk of the 6 KiB; record q / 12
-                    const uint32_t rr = q / 12, p = q - 12 * rr;  // chunk p of the record's 192-byte pair
-                    const uint32_t mk = uint32_t(__shfl(int(us.mask), int(32 * h + rr), 64));
-                    // whole 64-byte sectors only where a slot has parameters:
-                    // [0, 64) credential, [128, 192) verifier, [64, 128) either
-                    const bool need = p < 4 ? (mk & 1u) : (p >= 8 ? (mk & 2u) : mk != 0);
-                    if (r0 + rr < a.n && need) {
-                        const uint4 v = stg[q];
-                        __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst + q));
+                            d[q] = make_uint4(us.w[k][4 * q], us.w[k][4 * q + 1], us.w[k][4 * q + 2], us.w[k][4 * q + 3]);
                     }
                 }
             }
-            __syncthreads();                              // the window is reused below
-        } else if (us.mask) {
-            put_unix_direct(a.out.unix_params + 2 * i, us);
+            __syncthreads();
+            const uint32_t nq = 6 * min(kSlotPass, nslots - p0);
+            for (uint32_t q = t; q < nq; q += kDecTile) {
+                const uint4 v = stg[q];
+                __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, dst + 6 * p0 + q);
+            }
         }
+        __syncthreads();                              // the window is reused below
     }
     uint4* stage = reinterpret_cast<uint4*>(s_win);
 #pragma unroll

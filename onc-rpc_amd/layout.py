@@ -228,6 +228,33 @@ def describe(m, unix, auth_arena, payload_arena=None):
     return d
 
 
+def unix_used(msgs, status):
+    """(cred, verf) masks of the auths whose AUTH_UNIX parameters a decode
+    defines: OK records, kind UNIX, a credential of a call / a verifier of a
+    call or accepted reply."""
+    ok = status == 0
+    cred = ok & (msgs["msg_type"] == MSG_CALL) & ((msgs["cred_kind_len"] >> 24) == KIND_UNIX)
+    verf = ok & ((msgs["msg_type"] == MSG_CALL) | (msgs["reply_stat"] == REPLY_ACCEPTED)) & \
+        ((msgs["verf_kind_len"] >> 24) == KIND_UNIX)
+    return cred, verf
+
+
+def resolve_unix(msgs, unix, status):
+    """A decoded batch with its AUTH_UNIX slots resolved: (descriptors with
+    the unix refs zeroed, (n, 2, 96) bytes of each record's credential /
+    verifier parameters, zero where none). Two decodes that place the slots
+    differently (per-group packing of different batch partitions) agree on
+    this form exactly when they decoded the same messages."""
+    m = msgs.copy()
+    params = np.zeros((len(msgs), 2, UNIX_DTYPE.itemsize), np.uint8)
+    ub = unix.view(np.uint8).reshape(-1, UNIX_DTYPE.itemsize)
+    for k, (f, mask) in enumerate(zip(("cred", "verf"), unix_used(msgs, status))):
+        idx = np.nonzero(mask)[0]
+        params[idx, k] = ub[m[f + "_ref"][idx].astype(np.int64)]
+        m[f + "_ref"][idx] = 0
+    return m, params
+
+
 def records_from_wire(wire_list):
     """list of per-record byte strings -> (packed wire uint8 array, rec_off u64[n+1])."""
     lens = np.array([len(w) for w in wire_list], dtype=np.uint64)

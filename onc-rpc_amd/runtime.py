@@ -23,7 +23,7 @@ K_NAMES = ["enc_len_kernel", "scan_tiles_kernel", "enc_emit_kernel", "decode_ker
            "frame_counts_kernel", "frame_guess_kernel"]
 (K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY, K_IOV_LEN,
  K_IOV_EMIT, K_FRAME, K_FRAME_WRITE, K_FRAME_WALK, K_FRAME_COUNTS, K_FRAME_GUESS) = range(13)
-ABI_VERSION = 4
+ABI_VERSION = 5
 K_COUNT = len(K_NAMES)
 
 # every symbol include/onc_rpc.h declares

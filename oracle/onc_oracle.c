@@ -941,9 +941,30 @@ void oracle_encode_batch(uint64_t n, const onc_msg* msgs, const onc_unix_params*
     if (rec_off) rec_off[n] = off;
 }
 
+/* AUTH_UNIX slots (the library's output layout, include/onc_rpc.h
+ * onc_decoded): the OK records of each 64-record group [64g, 64g + 64) put
+ * their parameter sets in consecutive slots from 128g, in record order,
+ * credential before verifier; onc_auth.ref names the slot. `k` counts the
+ * group's slots so far (reset at every group start). */
+static void place_unix(uint64_t i, uint64_t* k, onc_msg* m, onc_unix_params* unix_params,
+                       const onc_unix_params u[2], int cred_unix, int verf_unix) {
+    if ((i & 63) == 0) *k = 0;
+    const uint64_t g = 2 * (i & ~(uint64_t)63);
+    if (cred_unix) {
+        m->cred.ref = g + *k;
+        unix_params[g + (*k)++] = u[0];
+    }
+    if (verf_unix) {
+        m->verf.ref = g + *k;
+        unix_params[g + (*k)++] = u[1];
+    }
+}
+
+/* lo is a multiple of 64 (or 0): groups are never split between calls */
 static void decode_range(const uint8_t* wire, const uint64_t* rec_off, uint64_t lo, uint64_t hi,
                          int mode, onc_msg* msgs, onc_unix_params* unix_params, int32_t* status,
                          uint32_t* aux0, uint32_t* aux1) {
+    uint64_t k = 0;
     for (uint64_t i = lo; i < hi; i++) {
         onc_unix_params u[2];
         memset(u, 0, sizeof(u));
@@ -951,13 +972,13 @@ static void decode_range(const uint8_t* wire, const uint64_t* rec_off, uint64_t 
         int32_t st = oracle_decode_message(wire, wire + a, b - a, mode, 2 * i, &msgs[i], u,
                                            &aux0[i], &aux1[i]);
         status[i] = st;
+        int cred_unix = 0, verf_unix = 0;
         if (st == ONC_OK) {
-            if (ONC_AUTH_KIND(msgs[i].cred) == ONC_KIND_UNIX && msgs[i].msg_type == ONC_MSG_CALL)
-                unix_params[2 * i] = u[0];
-            if (ONC_AUTH_KIND(msgs[i].verf) == ONC_KIND_UNIX &&
-                (msgs[i].msg_type == ONC_MSG_CALL || msgs[i].reply_stat == ONC_REPLY_ACCEPTED))
-                unix_params[2 * i + 1] = u[1];
+            cred_unix = ONC_AUTH_KIND(msgs[i].cred) == ONC_KIND_UNIX && msgs[i].msg_type == ONC_MSG_CALL;
+            verf_unix = ONC_AUTH_KIND(msgs[i].verf) == ONC_KIND_UNIX &&
+                        (msgs[i].msg_type == ONC_MSG_CALL || msgs[i].reply_stat == ONC_REPLY_ACCEPTED);
         }
+        place_unix(i, &k, &msgs[i], unix_params, u, cred_unix, verf_unix);
     }
 }
 
@@ -993,8 +1014,10 @@ void oracle_decode_batch_mt(const uint8_t* wire, const uint64_t* rec_off, uint64
     pthread_t tid[256];
     decode_job jobs[256];
     for (int t = 0; t < threads; t++) {
-        decode_job j = {wire, rec_off, n * t / threads, n * (t + 1) / threads, mode, msgs,
-                        unix_params, status, aux0, aux1};
+        /* whole 64-record groups per thread (place_unix) */
+        const uint64_t lo = (n * t / threads) & ~(uint64_t)63;
+        const uint64_t hi = t + 1 == threads ? n : (n * (t + 1) / threads) & ~(uint64_t)63;
+        decode_job j = {wire, rec_off, lo, hi, mode, msgs, unix_params, status, aux0, aux1};
         jobs[t] = j;
         pthread_create(&tid[t], NULL, decode_thread, &jobs[t]);
     }
@@ -1486,6 +1509,7 @@ void oracle_encode_body_batch(int root, uint64_t n, const onc_msg* msgs, const o
 void oracle_decode_body_batch(int root, const uint8_t* wire, const uint64_t* rec_off, uint64_t n, int mode,
                               const uint32_t* param, onc_msg* msgs, onc_unix_params* unix_params, int32_t* status,
                               uint32_t* aux0, uint32_t* aux1, uint32_t* consumed) {
+    uint64_t k = 0;
     for (uint64_t i = 0; i < n; i++) {
         onc_unix_params u[2];
         memset(u, 0, sizeof(u));
@@ -1493,13 +1517,13 @@ void oracle_decode_body_batch(int root, const uint8_t* wire, const uint64_t* rec
         int32_t st = oracle_decode_body(root, wire, wire + a, b - a, mode, param ? param[i] : 0, 2 * i, &msgs[i], u,
                                         &aux0[i], &aux1[i], &consumed[i]);
         status[i] = st;
+        int cred_unix = 0, verf_unix = 0;
         if (st == ONC_OK) {
-            int cred_unix = ONC_AUTH_KIND(msgs[i].cred) == ONC_KIND_UNIX && msgs[i].msg_type == ONC_MSG_CALL;
-            int verf_unix = ONC_AUTH_KIND(msgs[i].verf) == ONC_KIND_UNIX &&
-                            (msgs[i].msg_type == ONC_MSG_CALL || msgs[i].reply_stat == ONC_REPLY_ACCEPTED) &&
-                            root != ONC_ROOT_AUTH_FLAVOR && root != ONC_ROOT_AUTH_UNIX_PARAMS;
-            if (cred_unix) unix_params[2 * i] = u[0];
-            if (verf_unix) unix_params[2 * i + 1] = u[1];
+            cred_unix = ONC_AUTH_KIND(msgs[i].cred) == ONC_KIND_UNIX && msgs[i].msg_type == ONC_MSG_CALL;
+            verf_unix = ONC_AUTH_KIND(msgs[i].verf) == ONC_KIND_UNIX &&
+                        (msgs[i].msg_type == ONC_MSG_CALL || msgs[i].reply_stat == ONC_REPLY_ACCEPTED) &&
+                        root != ONC_ROOT_AUTH_FLAVOR && root != ONC_ROOT_AUTH_UNIX_PARAMS;
         }
+        place_unix(i, &k, &msgs[i], unix_params, u, cred_unix, verf_unix);
     }
 }

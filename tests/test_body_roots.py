@@ -186,7 +186,8 @@ def _slots(msgs, status):
     cred = ok & (msgs["msg_type"] == L.MSG_CALL) & ((msgs["cred_kind_len"] >> 24) == L.KIND_UNIX)
     verf = ok & ((msgs["msg_type"] == L.MSG_CALL) | (msgs["reply_stat"] == L.REPLY_ACCEPTED)) & \
         ((msgs["verf_kind_len"] >> 24) == L.KIND_UNIX)
-    return np.sort(np.concatenate([2 * np.nonzero(cred)[0], 2 * np.nonzero(verf)[0] + 1]))
+    # onc_auth.ref: packed per 64-record group (include/onc_rpc.h onc_decoded)
+    return np.sort(np.concatenate([msgs["cred_ref"][cred], msgs["verf_ref"][verf]]).astype(np.int64))
 
 
 def _assert_same_decode(g, o, what):
@@ -221,7 +222,7 @@ def _reencode_from_decoded(R, codec, root, w, dec):
     m, u, st, _, _, _ = dec
     keep = np.nonzero(st == 0)[0]
     hb = L.HostBatch(m[keep].copy(), u.copy() if len(u) else np.zeros(1, L.UNIX_DTYPE), w, w)
-    # unix refs stay the decoder's slot indices (2i / 2i + 1 of the original record)
+    # unix refs stay the decoder's slot indices (onc_auth.ref into the slot table)
     return R.encode_body_host_batch(codec, root, hb), keep
 
 
@@ -246,9 +247,10 @@ def test_gpu_body_golden_vectors(codec, R, oracle, golden, mode):
         if "data_len" in e:
             assert L.len_of(gm[i]["cred_kind_len"]) == e["data_len"]
         if "uid" in e:
-            assert int(gu[2 * i]["uid"]) == e["uid"]
+            assert int(gu[int(gm[i]["cred_ref"])]["uid"]) == e["uid"]
         if "machine_name" in e:
-            no, nl = int(gu[2 * i]["name_off"]), int(gu[2 * i]["name_len"])
+            u = gu[int(gm[i]["cred_ref"])]
+            no, nl = int(u["name_off"]), int(u["name_len"])
             assert bytes(w[no:no + nl]).hex() == e["machine_name"]
     (bw, boff, bst, blen), keep = _reencode_from_decoded(R, codec, L.ROOT_AUTH_FLAVOR, w, g)
     assert (bst == 0).all()
@@ -263,7 +265,7 @@ def test_gpu_body_golden_vectors(codec, R, oracle, golden, mode):
     _assert_same_decode(g, o, "unix_params vectors")
     gm, gu, gs, _, _, gc = g
     for i, v in enumerate(golden["unix_params"]):
-        e, u = v["expect"], gu[2 * i]
+        e, u = v["expect"], gu[int(gm[i]["cred_ref"])]
         ng = int(u["ngids"])
         got = {"stamp": int(u["stamp"]), "uid": int(u["uid"]), "gid": int(u["gid"]),
                "gids": [int(x) for x in u["gids"][:ng]],

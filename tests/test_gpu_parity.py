@@ -32,12 +32,13 @@ def R():
 
 
 def unix_slots_used(msgs, status):
-    """(slot index, mask) of AUTH_UNIX slots defined for OK records."""
+    """Indices of the AUTH_UNIX slots defined for OK records (onc_auth.ref;
+    packed per 64-record group, include/onc_rpc.h onc_decoded)."""
     ok = status == 0
     cred = ok & (msgs["msg_type"] == L.MSG_CALL) & ((msgs["cred_kind_len"] >> 24) == L.KIND_UNIX)
     verf = ok & ((msgs["msg_type"] == L.MSG_CALL) | (msgs["reply_stat"] == L.REPLY_ACCEPTED)) & \
         ((msgs["verf_kind_len"] >> 24) == L.KIND_UNIX)
-    idx = np.concatenate([2 * np.nonzero(cred)[0], 2 * np.nonzero(verf)[0] + 1])
+    idx = np.concatenate([msgs["cred_ref"][cred], msgs["verf_ref"][verf]]).astype(np.int64)
     return np.sort(idx)
 
 

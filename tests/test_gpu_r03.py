@@ -208,3 +208,53 @@ def test_chunked_encode_bit_exact(codec, R, oracle, shift, cap_frac):
     assert np.array_equal(rl.cpu().numpy().view(np.uint32), o_len)
     assert b[shift:shift + len(o_wire)].tobytes() == o_wire
     assert (b[:shift] == 0xA5).all() and (b[shift + cap:] == 0xA5).all()
+
+
+def _same_decode(g, o, what):
+    gm, gu, gs, ga0, ga1 = g
+    om, ou, os_, oa0, oa1 = o
+    bad = np.nonzero(gs != os_)[0]
+    assert len(bad) == 0, f"{what}: status at {bad[:8]} gpu {gs[bad[:8]]} oracle {os_[bad[:8]]}"
+    assert np.array_equal(ga0, oa0) and np.array_equal(ga1, oa1), what
+    # the packed AUTH_UNIX layout is the ABI's: descriptors (refs included)
+    # byte-equal, and the referenced slots equal
+    bad = np.nonzero((gm.view(np.uint8).reshape(-1, 64) != om.view(np.uint8).reshape(-1, 64)).any(axis=1))[0]
+    assert len(bad) == 0, f"{what}: descriptor at {bad[:8]}"
+    _, gp = L.resolve_unix(gm, gu, gs)
+    _, op = L.resolve_unix(om, ou, os_)
+    assert np.array_equal(gp, op), what
+
+
+@pytest.mark.parametrize("gen", ["mixed", "unix16"])
+def test_decode_at_every_record_alignment(codec, R, oracle, gen):
+    """The decode window's columns are funnelled by the record's byte offset
+    once, at staging (decode.hip `Rd`): the same batch decoded at wire
+    offsets 0..15 (every position in a 16-byte granule, every byte offset in
+    a word), and with 1..3-byte junk records between its records so that
+    neighbours start at every offset; both modes, bit-exact vs the oracle
+    (descriptors, AUTH_UNIX slots at their packed refs, statuses, aux)."""
+    if gen == "mixed":
+        hb = S.mixed(1500, seed=31, pmin=0, pmax=200, exotic=0.2)
+    else:
+        hb = S.call_unix16(1500, 40, seed=32)
+    wire, off, st, _ = oracle.encode_batch(hb)
+    assert (st == 0).all()
+    base = np.frombuffer(wire, np.uint8)
+    for shift in range(16):
+        w = np.concatenate([np.full(shift, 0xEE, np.uint8), base, np.zeros(16, np.uint8)])
+        o2 = off.astype(np.uint64) + np.uint64(shift)
+        for mode in (L.DECODE_SLICE, L.DECODE_BYTES):
+            _same_decode(R.decode_host_wire(codec, w, o2, mode), oracle.decode_batch(w, o2, mode),
+                         f"{gen} shift {shift} mode {mode}")
+    recs = []
+    for i in range(hb.n):
+        recs.append(bytes(base[int(off[i]):int(off[i + 1])]))
+        if i % 3 == 1:
+            recs.append(b"\x80" * (1 + (i // 3) % 3))   # IncompleteHeader, shifts what follows
+    w, o2 = L.records_from_wire(recs)
+    starts = np.asarray(o2[:-1], np.int64) & 15
+    assert len(np.unique(starts)) == 16
+    for mode in (L.DECODE_SLICE, L.DECODE_BYTES):
+        g = R.decode_host_wire(codec, w, o2, mode)
+        _same_decode(g, oracle.decode_batch(w, o2, mode), f"{gen} interleaved mode {mode}")
+        assert int((g[2] == 0).sum()) == hb.n
