@@ -233,6 +233,20 @@ struct ImgTile {
     uint8_t map[kMap2Cap];           // granule -> span record owning its first chunk
 };
 
+// Image slots are swizzled inside aligned groups of 8 (slot s lives at
+// s ^ ((s >> 3) & 7)). The header build writes one dword per lane per
+// instruction, lane = record, and records of one shape sit a fixed number of
+// slots apart: configs[0]'s 128-byte AUTH_UNIX headers are 8 slots = 32
+// dwords apart, so without the swizzle all 32 lanes of a ds_or_b32 lane
+// group hit one bank (bank = dword mod 32) — 32-way. With it, neighbouring
+// records' same word lands on 8 different chunk positions (4-way). The
+// swizzle stays inside a group of 8, so the capacity is unchanged.
+__device__ __forceinline__ int32_t img_slot(int32_t s) { return s ^ ((s >> 3) & 7); }
+__device__ __forceinline__ uint32_t img_dword(uint32_t d) {
+    return d ^ (((d >> 5) & 7u) << 2);
+}
+static_assert(kImgChunks % 8 == 0, "the slot swizzle permutes aligned groups of 8");
+
 // Header words of a record into the image at byte offset b (any alignment).
 // The image is zeroed per span and every record ORs its bytes in
 // (ds_or_b32): a dword shared with a neighbouring record (b & 3 != 0: the
@@ -242,17 +256,18 @@ struct ImgTile {
 // instantiated once.
 struct ImgSink {
     uint32_t* img32;
-    uint32_t d;        // image dword being produced
+    uint32_t d;        // image dword being produced (unswizzled)
     uint32_t sh;       // 32 - 8 * (b & 3)
     uint32_t prev;
     __device__ __forceinline__ void operator()(uint32_t w) {
         const uint32_t v = uint32_t(((uint64_t(w) << 32) | prev) >> sh);
-        __hip_atomic_fetch_or(img32 + d, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_or(img32 + img_dword(d), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         ++d;
         prev = w;
     }
     __device__ __forceinline__ void finish() {
-        if (sh != 32) __hip_atomic_fetch_or(img32 + d, prev >> sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        if (sh != 32)
+            __hip_atomic_fetch_or(img32 + img_dword(d), prev >> sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
 };
 
@@ -312,7 +327,7 @@ __device__ __forceinline__ ChunkPlan plan_chunk(const ImgTile& T, uint32_t gsh, 
     const uint4 q = T.pay[r];
     const int32_t s = c - (c >= m.z ? m.y : m.w);     // image slot: NP before the pure run, NP + its length after
     ChunkPlan P;
-    P.slot = s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s);
+    P.slot = img_slot(s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s));
     const uint32_t o = uint32_t(c) << 4;
     const bool hasp = q.x < q.y && o < q.y && o + 16 > q.x;
     const uint32_t x = max(q.x, min(o, q.y - 16));            // clamped window start
@@ -346,7 +361,7 @@ __device__ __forceinline__ ChunkPlan plan_chunk_interior(const ImgTile& T, uint3
     const uint4 q = T.pay[r];
     const int32_t s = c - (c >= m.z ? m.y : m.w);     // image slot: NP before the pure run, NP + its length after
     ChunkPlan P;
-    P.slot = s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s);
+    P.slot = img_slot(s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s));
     const uint32_t o = uint32_t(c) << 4;
     const bool hasp = o < q.y && o + 16 > q.x;          // kNoPay records: never
     const uint64_t sbase = uint64_t(q.z) | (uint64_t(q.w) << 32);
@@ -370,7 +385,7 @@ __device__ __forceinline__ ChunkPlan plan_chunk_full(const ImgTile& T, uint32_t 
     const uint4 q = T.pay[r];
     const int32_t s = c - (c >= m.z ? m.y : m.w);
     ChunkPlan P;
-    P.slot = s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s);
+    P.slot = img_slot(s < 0 ? 0 : (s >= kImgChunks ? kImgChunks - 1 : s));
     const uint32_t o = uint32_t(c) << 4;
     P.A = (uint64_t(q.z) | (uint64_t(q.w) << 32)) + B0 + o;
     P.sel = o - q.x;
@@ -564,7 +579,8 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         if (lo_rec) wave_lds_sync();                   // the previous span's readers are done
         // records OR into the image: zero the slots this span uses (the
         // cut above bounds them by kImgChunks)
-        const int used = int(min(uint64_t(kImgChunks), lane_u64(wnp, hi_rec - 1) - wbase + 1));
+        // (whole groups of 8: the swizzle permutes inside a group)
+        const int used = int(min(uint64_t(kImgChunks), (lane_u64(wnp, hi_rec - 1) - wbase + 8) & ~7ull));
         for (int k = lane; k < used; k += 64) T.img[k] = make_uint4(0, 0, 0, 0);
         const bool active = lane >= lo_rec && lane < hi_rec;
         const int j = lane - lo_rec;
@@ -769,7 +785,7 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
     const uint64_t S1 = lane_u64(Sen, hi_rec - 1);
     const int64_t C0 = int64_t(S0 >> 4);
     const uint64_t B0 = uint64_t(C0) << 4;
-    const int used = int(min(uint64_t(kImgChunks), lane_u64(Swnp, hi_rec - 1) - wbase + 1));
+    const int used = int(min(uint64_t(kImgChunks), (lane_u64(Swnp, hi_rec - 1) - wbase + 8) & ~7ull));
     for (int k = lane; k < used; k += 64) W.T.img[k] = make_uint4(0, 0, 0, 0);
     const bool active = lane >= lo_rec && lane < hi_rec;
     const int j = lane - lo_rec;
