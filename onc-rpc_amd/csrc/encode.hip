@@ -1055,15 +1055,10 @@ __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
 #endif
 }
 
-// kNT: bit 0 = nontemporal payload loads, bit 1 = nontemporal stores (a
-// measured alternative, header chunks stored temporally so that the decoder
-// finds them cached, made the decode slower: 60 -> 69 us on c1, the dirty
-// lines are written back at the kernel boundary);
-// kOcc: workgroups per CU the register allocation must allow (0 = free)
 // kNT: bit 0 = nontemporal payload loads, bit 1 = nontemporal stores (header
 // chunks stored temporally so that the decoder finds them cached made the
 // decode slower, 60 -> 69 us on c1: the dirty lines are written back at the
-// kernel boundary). Registers are left free (106 VGPRs, 4 waves per SIMD):
+// kernel boundary). Registers are left free (102 VGPRs, 4 waves per SIMD):
 // squeezed to 5 waves per SIMD every shape measured slower (spills).
 template <int kU, int kNT = 0, bool kFused = false, bool kRoot = false>
 __global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) {
