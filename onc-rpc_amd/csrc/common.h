@@ -256,22 +256,30 @@ struct ShiftSink {
     __device__ __forceinline__ void finish() { *dst = funnel(prev, 0u, sh); }
 };
 
-// AuthUnixParams::serialise_into (unix_params.rs:162-176) of unix-table
-// entry `ref`, preceded (kLen) by its serialised_len — the opaque length
-// AuthFlavor::serialise_into writes before it (flavor.rs:123-126).
-template <bool kLen, class Sink>
-__device__ __forceinline__ void put_unix_words(uint64_t ref, const EncSrc& s, Sink& out) {
+// The whole 96-byte parameter block of unix-table entry `ref` in six dwordx4
+// loads issued together (one memory round trip; field by field, each gid was
+// a dependent load between two sink writes).
+struct UnixRegs {
+    u32x4 q[6];
+};
+__device__ __forceinline__ UnixRegs issue_unix(const onc_unix_params* unix, uint64_t ref) {
     static_assert(sizeof(onc_unix_params) == 96 && offsetof(onc_unix_params, ngids) == 12 &&
                       offsetof(onc_unix_params, name_off) == 16 && offsetof(onc_unix_params, name_len) == 24 &&
                       offsetof(onc_unix_params, gids) == 32,
-                  "parameter block layout read below");
-    // the whole 96-byte parameter block in six dwordx4 loads issued together
-    // (one memory round trip; field by field, each gid was a dependent load
-    // between two sink writes)
-    const uintptr_t ua = reinterpret_cast<uintptr_t>(s.unix + ref);
-    u32x4 q[6];
+                  "parameter block layout read by put_unix_words");
+    const uintptr_t ua = reinterpret_cast<uintptr_t>(unix + ref);
+    UnixRegs u;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) q[k] = gload<u32x4>(ua + 16 * k);
+    for (int k = 0; k < 6; ++k) u.q[k] = gload<u32x4>(ua + 16 * k);
+    return u;
+}
+
+// AuthUnixParams::serialise_into (unix_params.rs:162-176) of a loaded
+// parameter block, preceded (kLen) by its serialised_len — the opaque length
+// AuthFlavor::serialise_into writes before it (flavor.rs:123-126).
+template <bool kLen, class Sink>
+__device__ __forceinline__ void put_unix_words(const UnixRegs& u, const EncSrc& s, Sink& out) {
+    const u32x4* q = u.q;
     const uint32_t stamp = q[0].x, uid = q[0].y, gid = q[0].z, ng = q[0].w;
     const uint64_t name_off = uint64_t(q[1].x) | (uint64_t(q[1].y) << 32);
     const uint32_t nl = q[1].z;
@@ -290,6 +298,12 @@ __device__ __forceinline__ void put_unix_words(uint64_t ref, const EncSrc& s, Si
         if (j < ng) out(bswap(gids[j]));
 }
 
+// ... of unix-table entry `ref`
+template <bool kLen, class Sink>
+__device__ __forceinline__ void put_unix_words(uint64_t ref, const EncSrc& s, Sink& out) {
+    put_unix_words<kLen>(issue_unix(s.unix, ref), s, out);
+}
+
 // Opaque::serialise_into (opaque.rs:38-56) of an auth body: length, body
 // words, the last one zero padded.
 template <class Sink>
@@ -301,25 +315,30 @@ __device__ __forceinline__ void put_opaque_words(const onc_auth& a, const EncSrc
 }
 
 // AuthFlavor::serialise_into (flavor.rs:106-129).
+// (pre: the auth's parameter block, already loaded — an AUTH_UNIX credential
+// whose block the caller issued with its other loads)
 template <class Sink>
-__device__ __forceinline__ void put_auth_words(const onc_auth& a, const EncSrc& s, Sink& out) {
+__device__ __forceinline__ void put_auth_words(const onc_auth& a, const EncSrc& s, Sink& out,
+                                               const UnixRegs* pre = nullptr, bool use_pre = false) {
     const uint32_t kind = a.kind_len >> 24;
     out(bswap(kind == ONC_KIND_UNKNOWN ? a.id : kind));
     if (kind != ONC_KIND_UNIX) {
         put_opaque_words(a, s, out);
         return;
     }
-    put_unix_words<true>(a.ref, s, out);
+    if (use_pre) put_unix_words<true>(*pre, s, out);
+    else put_unix_words<true>(a.ref, s, out);
 }
 
 // CallBody::serialise_into (call_body.rs:98-108) up to the raw payload.
 template <class Sink>
-__device__ __forceinline__ void put_call_words(const onc_msg& d, const EncSrc& s, Sink& out) {
+__device__ __forceinline__ void put_call_words(const onc_msg& d, const EncSrc& s, Sink& out,
+                                               const UnixRegs* cred_pre = nullptr, bool use_pre = false) {
     out(bswap(2u));                           // RPC_VERSION call_body.rs:10
     out(bswap(d.u.call.program));
     out(bswap(d.u.call.program_version));
     out(bswap(d.u.call.procedure));
-    put_auth_words(d.cred, s, out);
+    put_auth_words(d.cred, s, out, cred_pre, use_pre);
     put_auth_words(d.verf, s, out);
 }
 
@@ -361,12 +380,14 @@ __device__ __forceinline__ void put_reply_words(const onc_msg& d, const EncSrc& 
 
 // RpcMessage::serialise_into (rpc_message.rs:136-164; MessageType :55-68)
 // up to the raw payload.
+// (cred_pre, when use_pre: the Call's AUTH_UNIX credential block, already loaded)
 template <class Sink>
-__device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, Sink& out) {
+__device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, Sink& out,
+                                                 const UnixRegs* cred_pre = nullptr, bool use_pre = false) {
     out(bswap((len - 4u) | 0x80000000u));        // record mark, rpc_message.rs:156
     out(bswap(d.xid));
     out(bswap(uint32_t(d.msg_type)));
-    if (d.msg_type == ONC_MSG_CALL) put_call_words(d, s, out);
+    if (d.msg_type == ONC_MSG_CALL) put_call_words(d, s, out, cred_pre, use_pre);
     else put_reply_words(d, s, out);
 }
 

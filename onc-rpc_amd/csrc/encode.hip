@@ -497,7 +497,7 @@ __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, 
     }
 }
 
-template <int kU, int kNT, bool kFused, bool kRoot = false, bool kGiven = false>
+template <int kU, int kNT, bool kFused, bool kRoot = false, bool kGiven = false, bool kPre = false>
 __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile, uint64_t given = 0) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = tile * kEmitRecs;
@@ -527,6 +527,10 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     uint64_t len = 0, poff = 0;
     uint32_t hw = 0;
     bool word_aligned = true;
+    // a Call's AUTH_UNIX credential: its parameter block is issued with the
+    // header build's descriptor reload (one round trip, not two dependent)
+    const bool cred_unix = kPre && !kRoot && dm.msg_type == ONC_MSG_CALL && (dm.cred.kind_len >> 24) == ONC_KIND_UNIX;
+    const uint64_t cred_ref = dm.cred.ref;
     if (lane < nrec) {
         const onc_msg& d = dm;
         // the same function as enc_len: lengths agree
@@ -604,12 +608,18 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                 // reloaded (an L2 hit) rather than kept live across the span
                 // loop (kept live: 162 VGPRs, 3 waves per SIMD)
                 MsgRegs mr2 = issue_msg(a.msgs + r0 + lane);
+                UnixRegs cq;
+                if (cred_unix) {
+                    cq = issue_unix(a.unix, cred_ref);    // validated by plan_record (len != 0)
+                    asm volatile("" : "+v"(cq.q[0]), "+v"(cq.q[1]), "+v"(cq.q[2]), "+v"(cq.q[3]), "+v"(cq.q[4]),
+                                 "+v"(cq.q[5]));
+                }
                 asm volatile("" : "+v"(mr2.q[0]), "+v"(mr2.q[1]), "+v"(mr2.q[2]), "+v"(mr2.q[3]));
                 const onc_msg d = as_msg(mr2);
                 const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
                 ImgSink w{img32, uint32_t(ibb >> 2), 32u - 8u * uint32_t(ibb & 3), 0u};
                 if (kRoot) put_root_words(d, uint32_t(len), src, a.root, w);
-                else put_header_words(d, uint32_t(len), src, w);
+                else put_header_words(d, uint32_t(len), src, w, &cq, cred_unix);
                 if (small) {
                     // all of it lies in non-pure chunks (np = 0): right after
                     // the header (bytes past its end read as zero)
@@ -1065,7 +1075,7 @@ __global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) 
     __shared__ ImgTile s_tiles[kFastWaves];
     const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
     if (tile < num_emit_tiles(a.n))
-        enc_emit_tile<kU, kNT, kFused, kRoot>(a, s_tiles[threadIdx.x >> 6], tile);
+        enc_emit_tile<kU, kNT, kFused, kRoot, false, !kRoot>(a, s_tiles[threadIdx.x >> 6], tile);
 }
 
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
