@@ -21,6 +21,11 @@ struct onc_codec {
     uint64_t* scratch = nullptr;
     uint64_t scratch_tiles = 0;
     uint8_t* frame_scratch = nullptr;   // onc_frame_stream per-chunk state
+    // decode first-round policy (decode.hip kLine): a sampled workgroup's
+    // count of records that needed a second round, written by the decode
+    // into mapped host memory and read here at the next launch
+    uint32_t* dec_hint_host = nullptr;
+    uint32_t* dec_hint_dev = nullptr;
     uint64_t frame_chunks = 0;
     uint64_t frame_chunk = onc::kFrameChunkDefault;   // ONC_RPC_FRAME_CHUNK at create (bytes, >= 64)
     uint64_t enc_chunk = 0;    // ONC_RPC_ENC_CHUNK at create (records, multiple of 1024; 0 = kEncChunk)
@@ -140,6 +145,17 @@ int set_device(onc_codec* c) {
     return ONC_RC_OK;
 }
 
+// The message decode's first-round policy from the previous launch's sample
+// (a plain read of mapped host memory: no synchronisation, at worst one
+// launch stale); variant bits 0x80000 / 0x100000 force it.
+void set_decode_policy(onc_codec* c, onc::DecArgs& a) {
+    a.hint = c->dec_hint_dev;
+    const uint32_t seen = *reinterpret_cast<volatile uint32_t*>(c->dec_hint_host);
+    a.line = seen >= onc::kLine1Min ? 1u : 0u;
+    if (c->variant & 0x80000) a.line = 1;
+    if (c->variant & 0x100000) a.line = 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -169,6 +185,14 @@ int onc_codec_create(onc_codec** out, int device, void* hip_stream) {
         delete c;
         return ONC_RC_EHIP;
     }
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->dec_hint_host), 256, hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&c->dec_hint_dev), c->dec_hint_host, 0) != hipSuccess) {
+        if (c->dec_hint_host) (void)hipHostFree(c->dec_hint_host);
+        delete c;
+        return ONC_RC_ENOMEM;
+    }
+    *c->dec_hint_host = 0;
     *out = c;
     return ONC_RC_OK;
 }
@@ -184,6 +208,7 @@ int onc_codec_destroy(onc_codec* c) {
     for (auto e : c->spare) (void)hipEventDestroy(e);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->frame_scratch) (void)hipFree(c->frame_scratch);
+    if (c->dec_hint_host) (void)hipHostFree(c->dec_hint_host);
     delete c;
     return ONC_RC_OK;
 }
@@ -647,6 +672,7 @@ int onc_decode(onc_codec* c, const uint8_t* wire, const uint64_t* rec_off, uint6
     a.rec_off = rec_off;
     a.out = *out;
     a.variant = c->variant;
+    set_decode_policy(c, a);
     return run(c, ONC_K_DEC_PARSE, "decode", [&] { return onc::launch_decode(a, mode, c->stream); });
 }
 
@@ -669,6 +695,7 @@ int onc_decode_lengths(onc_codec* c, const uint8_t* wire, const uint32_t* rec_le
     a.wire = wire;
     a.out = *out;
     a.variant = c->variant;
+    set_decode_policy(c, a);
     a.rec_len = rec_len;
     a.tile_sum = c->scratch;
     a.blk_sum = c->scratch + 3 * T;

@@ -30,8 +30,10 @@ namespace onc {
 #ifndef ONC_DEC_WIN
 #define ONC_DEC_WIN 10
 #endif
-constexpr uint32_t kWin1 = ONC_DEC_WIN < 4 ? ONC_DEC_WIN : 4;
+constexpr uint32_t kWin1 = 4;                 // round-1 chunks (standard policy)
+constexpr uint32_t kWin1L = 8;                // round-1 chunks at most (line policy, decode_kernel)
 constexpr uint32_t kWinChunks = ONC_DEC_WIN;
+static_assert(kWinChunks >= kWin1L, "round 1 stays inside the window");
 constexpr uint32_t kWinWords = 4 * kWinChunks;
 #ifndef ONC_DEC_TILE
 #define ONC_DEC_TILE 64     // c1 decode 54.7 -> 50.2 us, c2 81 -> 78.6, c3 447 -> 468 vs 256 (profiles/lab_r02_dec_tile.log)
@@ -497,8 +499,144 @@ static_assert(kDecTile == 64, "kFromLen: one wave per workgroup, 64 workgroup to
 // kRoot (onc_decode_body): a.root selects the decoded type; the window
 // takes the record's first kWinChunks chunks in two rounds (the header-extent
 // guess below is the RpcMessage layout's).
+// The line policy (message decode, kLine). A header longer than the first
+// round re-fetches, in round 2, the 128-byte line round 1 read — by then that
+// line has left L2 (configs[3]: 128-byte AUTH_UNIX headers 1152 bytes apart,
+// 270 B fetched per record for one line of header). Round 1 can instead take
+// the rest of the record's first line (no extra line): that saves the second
+// fetch when headers are long and costs load issue when they are not — the
+// decode's time follows its scattered load instructions (c3 decode 367 -> 257
+// us, c0 85 -> 80, but c1 50.5 -> 64.5, c2 58 -> 61;
+// profiles/lab_r03_decode_line.log). So the policy is chosen per launch
+// (codec.hip launch_decode) from the records the previous launch on the same
+// codec saw: every 64th workgroup stores how many of its 64 records needed a
+// second round under the standard policy into the codec's hint word, which
+// lives in mapped host memory, so the host reads it at the next launch
+// without a synchronisation and launches the kernel instance of that policy
+// (kLine1Min, kernels.h; break-even measured at ~1/3) — no policy code in
+// either kernel. A device-memory word read by every workgroup cost the c1
+// decode 1-2 us of prologue; results never depend on the policy (only which
+// chunks each round loads); variant bits 0x80000 / 0x100000 force the line /
+// the standard policy (tests).
+
+// The window of one record (L != 0): round 1, the header extent, round 2.
+// Returns the chunks staged in LDS; needs2: the header reaches past the
+// standard policy's first round. kLine: the line policy (decode_kernel).
+template <bool kLine, bool kPolicy, bool kRoot>
+__device__ __forceinline__ uint32_t stage_window(uint32_t* s_win, int t, uintptr_t base, uintptr_t win, uint32_t q0,
+                                                 uint32_t d0, uint64_t L, bool& needs2) {
+    const uint32_t avail = uint32_t(min(uint64_t(kWinChunks), (q0 + L + 15) >> 4));
+    const uint32_t r44 = kPolicy ? uint32_t(min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4)) : kWin1;
+    // line policy: also the rest of the record's first 128-byte line
+    const uint32_t rln = uint32_t((((win | 127u) + 1u) - win) >> 4);
+    const uint32_t r1 = kLine ? min(kWin1L, max(r44, rln)) : r44;
+    uint32_t nch = min(r1, avail);
+    // all round-1 loads issued without a per-chunk branch (chunks past
+    // the record's last granule re-read that granule) and pinned: under
+    // branches the compiler waited for chunk 2 before issuing chunk 3
+    u32x4 v[kWin1L];
+    const uintptr_t last = win + 16 * (nch - 1);          // nch >= 1 here (L != 0)
+#pragma unroll
+    for (uint32_t j = 0; j < kWin1; ++j) v[j] = gload<u32x4>(min(win + 16 * j, last));
+    static_assert(kWin1 == 4 && kWin1L == 8, "pin lists below");
+    if constexpr (kLine) {
+#pragma unroll
+        for (uint32_t j = kWin1; j < kWin1L; ++j) v[j] = gload<u32x4>(min(win + 16 * j, last));
+        asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                     "+v"(v[7]));
+    } else {
+        asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+#pragma unroll
+        for (uint32_t j = kWin1; j < kWin1L; ++j) v[j] = u32x4{0u, 0u, 0u, 0u};
+    }
+    // column word c = record bytes [4c, 4c + 4): loaded words d0 + c and
+    // d0 + c + 1 funnelled by the record's byte offset in its dword. The
+    // last word of the round (its upper bytes in the next chunk) is
+    // rewritten if round 2 loads that chunk; otherwise it lies past `lim`.
+    const uint32_t sh = q0 & 3u;
+    uint32_t e[4 * kWin1L + 1];
+#pragma unroll
+    for (uint32_t j = 0; j < kWin1L; ++j) {
+        e[4 * j] = v[j].x;
+        e[4 * j + 1] = v[j].y;
+        e[4 * j + 2] = v[j].z;
+        e[4 * j + 3] = v[j].w;
+    }
+    e[4 * kWin1L] = 0u;
+#pragma unroll
+    for (uint32_t r = 0; r < 4 * kWin1; ++r)
+        if (r >= d0 && r < 4 * nch) s_win[(r - d0) * kDecTile + t] = funnel(e[r], e[r + 1], sh);
+    if constexpr (kLine) {
+#pragma unroll
+        for (uint32_t r = 4 * kWin1; r < 4 * kWin1L; ++r)       // r >= 16 > d0
+            if (r < 4 * nch) s_win[(r - d0) * kDecTile + t] = funnel(e[r], e[r + 1], sh);
+    }
+    // Header extent from the first round: call -> 36 + cred body + verf
+    // flavor/length + the verifier body (its length when the first round
+    // holds it, else a 16-byte guess); reply -> up to 12 bytes past an
+    // accepted verifier.
+    const Rd R1{base, 16 * nch - q0, &s_win[t]};
+    uint32_t need = uint32_t(min(L, uint64_t(16 * kWinChunks)));
+    if (!kRoot && L >= 36 && 16 * nch >= q0 + 36) {
+        const uint32_t mt = R1.be32(8);
+        if (mt == ONC_MSG_CALL) {
+            const uint32_t cl = R1.be32(32);
+            const uint32_t vpos = 36 + cl + pad4(cl) + 4;      // verifier length field
+            if (cl > ONC_MAX_AUTH_LEN) {
+                need = 36;
+            } else if (q0 + vpos + 4 <= 16 * nch && vpos + 4 <= L) {
+                const uint32_t vl = R1.be32(vpos);
+                need = vpos + 4 + (vl <= ONC_MAX_AUTH_LEN ? vl + pad4(vl) : 0);
+            } else {
+                need = vpos + 4 + 16;
+            }
+        } else if (mt == ONC_MSG_REPLY) {
+            const uint32_t vl = R1.be32(20);
+            need = vl <= ONC_MAX_AUTH_LEN ? 24 + vl + pad4(vl) + 12 : 24;
+        }
+    }
+    const uint32_t want = min(avail, (q0 + need + 15) >> 4);
+    needs2 = want > min(r44, avail);
+    if (want > nch) {
+        // chunks [nch, want): from kR2 on (the first chunk round 1 may
+        // have skipped) up to the window's end
+        constexpr uint32_t kR2 = kPolicy ? 3u : kWin1;   // round 1 held >= 3 chunks if L >= 44
+        constexpr uint32_t kN2 = kWinChunks > kR2 ? kWinChunks - kR2 : 1;
+        u32x4 w[kN2];
+#pragma unroll
+        for (uint32_t j = 0; j < kN2; ++j) w[j] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (uint32_t j = kR2; j < kWinChunks; ++j)
+            if (j >= nch && j < want) w[j - kR2] = gload<u32x4>(win + 16 * j);
+        uint32_t f[4 * kN2 + 1];
+#pragma unroll
+        for (uint32_t j = 0; j < kN2; ++j) {
+            f[4 * j] = w[j].x;
+            f[4 * j + 1] = w[j].y;
+            f[4 * j + 2] = w[j].z;
+            f[4 * j + 3] = w[j].w;
+        }
+        f[4 * kN2] = 0u;
+#pragma unroll
+        for (uint32_t r = 4 * kR2; r < 4 * kWinChunks; ++r)       // r >= 12 > d0
+            if (r >= 4 * nch && r < 4 * want) s_win[(r - d0) * kDecTile + t] = funnel(f[r - 4 * kR2], f[r - 4 * kR2 + 1], sh);
+        // round 1's last word, now with its upper bytes (nch >= kR2 here)
+        uint32_t lo = e[4 * kWin1L - 1], hi = w[0].x;
+#pragma unroll
+        for (uint32_t c = kR2; c < kWin1L; ++c)
+            if (nch == c) {
+                lo = e[4 * c - 1];
+                hi = w[c - kR2].x;
+            }
+        if (nch == kWin1L && kWin1L - kR2 < kN2) hi = w[kWin1L - kR2].x;
+        s_win[(4 * nch - 1 - d0) * kDecTile + t] = funnel(lo, hi, sh);
+        nch = want;
+    }
+    return nch;
+}
+
 template <int MODE, bool kExact = false, bool kNTOut = false, bool kFromLen = false, bool kBlkFused = false,
-          bool kRoot = false>
+          bool kRoot = false, bool kLine = false>
 __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     __shared__ uint32_t s_win[kWinWords * kDecTile];
     static_assert(kWinWords * kDecTile * 4 >= kDecTile * sizeof(onc_msg), "descriptor staging reuses the window");
@@ -506,6 +644,8 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     const uint64_t i0 = uint64_t(blockIdx.x) * kDecTile;
     const uint64_t i = i0 + t;
     const bool valid = i < a.n;
+    constexpr bool kPolicy = kExact && !kRoot;
+    bool needs2 = false;                           // a second round under the standard policy
     uint64_t b = 0, L = 0;
     if constexpr (kFromLen) {
         const uint64_t wg = blockIdx.x;
@@ -560,95 +700,14 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     // empty records read nothing.
     uint32_t nch = 0;
     if (L != 0) {
-        const uint32_t avail = uint32_t(min(uint64_t(kWinChunks), (q0 + L + 15) >> 4));
-        const uint32_t r1 = kExact && !kRoot ? uint32_t(min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4)) : kWin1;
-        nch = min(r1, avail);
-        // all kWin1 loads issued without a per-chunk branch (chunks past the
-        // record's last granule re-read that granule) and pinned: under
-        // branches the compiler waited for chunk 2 before issuing chunk 3
-        u32x4 v[kWin1];
-        const uintptr_t last = win + 16 * (nch - 1);          // nch >= 1 here (L != 0)
-#pragma unroll
-        for (uint32_t j = 0; j < kWin1; ++j) v[j] = gload<u32x4>(min(win + 16 * j, last));
-        static_assert(kWin1 == 4, "pin list below");
-        asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
-        // column word c = record bytes [4c, 4c + 4): loaded words d0 + c and
-        // d0 + c + 1 funnelled by the record's byte offset in its dword. The
-        // last word of the round (its upper bytes in the next chunk) is
-        // rewritten if round 2 loads that chunk; otherwise it lies past `lim`.
-        const uint32_t sh = q0 & 3u;
-        uint32_t e[4 * kWin1 + 1];
-#pragma unroll
-        for (uint32_t j = 0; j < kWin1; ++j) {
-            e[4 * j] = v[j].x;
-            e[4 * j + 1] = v[j].y;
-            e[4 * j + 2] = v[j].z;
-            e[4 * j + 3] = v[j].w;
-        }
-        e[4 * kWin1] = 0u;
-#pragma unroll
-        for (uint32_t r = 0; r < 4 * kWin1; ++r)
-            if (r >= d0 && r < 4 * nch) s_win[(r - d0) * kDecTile + t] = funnel(e[r], e[r + 1], sh);
-        // Header extent from the first round: call -> 36 + cred body + verf
-        // flavor/length + the verifier body (its length when the first round
-        // holds it, else a 16-byte guess); reply -> up to 12 bytes past an
-        // accepted verifier.
-        const Rd R1{base, 16 * nch - q0, &s_win[t]};
-        uint32_t need = uint32_t(min(L, uint64_t(16 * kWinChunks)));
-        if (!kRoot && L >= 36 && 16 * nch >= q0 + 36) {
-            const uint32_t mt = R1.be32(8);
-            if (mt == ONC_MSG_CALL) {
-                const uint32_t cl = R1.be32(32);
-                const uint32_t vpos = 36 + cl + pad4(cl) + 4;      // verifier length field
-                if (cl > ONC_MAX_AUTH_LEN) {
-                    need = 36;
-                } else if (q0 + vpos + 4 <= 16 * nch && vpos + 4 <= L) {
-                    const uint32_t vl = R1.be32(vpos);
-                    need = vpos + 4 + (vl <= ONC_MAX_AUTH_LEN ? vl + pad4(vl) : 0);
-                } else {
-                    need = vpos + 4 + 16;
-                }
-            } else if (mt == ONC_MSG_REPLY) {
-                const uint32_t vl = R1.be32(20);
-                need = vl <= ONC_MAX_AUTH_LEN ? 24 + vl + pad4(vl) + 12 : 24;
-            }
-        }
-        const uint32_t want = min(avail, (q0 + need + 15) >> 4);
-        if (want > nch) {
-            // chunks [nch, want): from kR2 on (the first chunk round 1 may
-            // have skipped) up to the window's end
-            constexpr uint32_t kR2 = kExact && !kRoot ? 3u : kWin1;   // round 1 held >= 3 chunks if L >= 44
-            constexpr uint32_t kN2 = kWinChunks > kR2 ? kWinChunks - kR2 : 1;
-            u32x4 w[kN2];
-#pragma unroll
-            for (uint32_t j = 0; j < kN2; ++j) w[j] = u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-            for (uint32_t j = kR2; j < kWinChunks; ++j)
-                if (j >= nch && j < want) w[j - kR2] = gload<u32x4>(win + 16 * j);
-            uint32_t f[4 * kN2 + 1];
-#pragma unroll
-            for (uint32_t j = 0; j < kN2; ++j) {
-                f[4 * j] = w[j].x;
-                f[4 * j + 1] = w[j].y;
-                f[4 * j + 2] = w[j].z;
-                f[4 * j + 3] = w[j].w;
-            }
-            f[4 * kN2] = 0u;
-#pragma unroll
-            for (uint32_t r = 4 * kR2; r < 4 * kWinChunks; ++r)       // r >= 12 > d0
-                if (r >= 4 * nch && r < 4 * want) s_win[(r - d0) * kDecTile + t] = funnel(f[r - 4 * kR2], f[r - 4 * kR2 + 1], sh);
-            // round 1's last word, now with its upper bytes (nch >= kR2 here)
-            uint32_t lo = e[4 * kWin1 - 1], hi = w[0].x;
-#pragma unroll
-            for (uint32_t c = kR2; c < kWin1; ++c)
-                if (nch == c) {
-                    lo = e[4 * c - 1];
-                    hi = w[c - kR2].x;
-                }
-            if (nch == kWin1 && kWin1 - kR2 < kN2) hi = w[kWin1 - kR2].x;
-            s_win[(4 * nch - 1 - d0) * kDecTile + t] = funnel(lo, hi, sh);
-            nch = want;
-        }
+        nch = stage_window<kLine && kPolicy, kPolicy, kRoot>(s_win, t, base, win, q0, d0, L, needs2);
+    }
+    if constexpr (kPolicy) {
+        // every 64th workgroup reports for the next launch how many of its
+        // records needed a second round under the standard policy
+        const uint32_t cnt = uint32_t(__popcll(__ballot(needs2)));
+        if (a.hint && (blockIdx.x & 63) == 0 && t == 0)
+            __hip_atomic_store(a.hint, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     const uint32_t lim = nch ? 16 * nch - q0 : 0u;
     const Rd R{base, lim, &s_win[t]};
@@ -789,6 +848,30 @@ hipError_t launch_dlen_tiles(const uint32_t* rec_len, uint64_t n, uint64_t* tile
     return hipGetLastError();
 }
 
+// The message decode (onc_decode / onc_decode_lengths) under one first-round
+// policy (kLine, decode_kernel).
+template <bool kLine>
+hipError_t launch_message_decode(const DecArgs& a, int mode, hipStream_t s) {
+    const uint64_t wgs = (a.n + kDecTile - 1) / kDecTile;
+    const dim3 g{uint32_t(wgs)}, b{uint32_t(kDecTile)};
+    if (a.rec_len) {
+        const bool fused = a.blk_base == nullptr;
+        if (mode == ONC_DECODE_BYTES) {
+            if (fused) ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true, true, true, false, kLine>), g, b, 0, s, a);
+            else ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true, true, false, false, kLine>), g, b, 0, s, a);
+        } else {
+            if (fused) ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true, true, true, false, kLine>), g, b, 0, s, a);
+            else ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true, true, false, false, kLine>), g, b, 0, s, a);
+        }
+        return hipGetLastError();
+    }
+    if (mode == ONC_DECODE_BYTES)
+        ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true, false, false, false, kLine>), g, b, 0, s, a);
+    else
+        ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true, false, false, false, kLine>), g, b, 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s) {
     if (a.body) {
         const uint64_t tiles = (a.n + kDecTile - 1) / kDecTile;
@@ -800,24 +883,8 @@ hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s) {
                        dim3(kDecTile), 0, s, a);
         return hipGetLastError();
     }
-    if (a.rec_len) {
-        const uint64_t wgs = (a.n + kDecTile - 1) / kDecTile;
-        const bool fused = a.blk_base == nullptr;
-        if (mode == ONC_DECODE_BYTES) {
-            if (fused) ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true, true, true>), dim3(uint32_t(wgs)), dim3(kDecTile), 0, s, a);
-            else ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true, true, false>), dim3(uint32_t(wgs)), dim3(kDecTile), 0, s, a);
-        } else {
-            if (fused) ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true, true, true>), dim3(uint32_t(wgs)), dim3(kDecTile), 0, s, a);
-            else ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true, true, false>), dim3(uint32_t(wgs)), dim3(kDecTile), 0, s, a);
-        }
-        return hipGetLastError();
-    }
-    const uint64_t tiles = (a.n + kDecTile - 1) / kDecTile;
-    if (mode == ONC_DECODE_BYTES)
-        ONC_LAUNCH((decode_kernel<ONC_DECODE_BYTES, true, true>), dim3(uint32_t(tiles)), dim3(kDecTile), 0, s, a);
-    else
-        ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true>), dim3(uint32_t(tiles)), dim3(kDecTile), 0, s, a);
-    return hipGetLastError();
+    if (a.line) return launch_message_decode<true>(a, mode, s);
+    return launch_message_decode<false>(a, mode, s);
 }
 
 }  // namespace onc

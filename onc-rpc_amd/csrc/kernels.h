@@ -134,7 +134,12 @@ struct DecArgs {
     uint32_t root;              // ONC_ROOT_*; ONC_ROOT_RPC_MESSAGE = the product decode
     const uint32_t* param;      // per record: expected_len / max_len (or NULL)
     uint32_t* consumed;         // optional: bytes the decoded value occupies
+    uint32_t* hint;             // the codec's policy word (mapped host memory; decode.hip kLine) or NULL
+    uint32_t line;              // message decode: the line policy (decode.hip kLine)
 };
+// the line policy when at least this many of a sampled workgroup's 64
+// records needed a second first-round window under the standard one
+constexpr uint32_t kLine1Min = 24;
 constexpr uint64_t kDecLenBlk = 4096;          // records per length block
 constexpr uint64_t kDecLenFusedBlocks = 512;   // up to 2M records: block totals summed in the decode
 

@@ -258,3 +258,55 @@ def test_decode_at_every_record_alignment(codec, R, oracle, gen):
         g = R.decode_host_wire(codec, w, o2, mode)
         _same_decode(g, oracle.decode_batch(w, o2, mode), f"{gen} interleaved mode {mode}")
         assert int((g[2] == 0).sum()) == hb.n
+
+
+@pytest.mark.parametrize("variant", [0, 0x80000, 0x100000])
+def test_decode_line_policy(R, oracle, monkeypatch, variant):
+    """The decode's two first-round policies (decode.hip kLine1Min): the line
+    policy (0x80000: round 1 takes the rest of the record's first 128-byte
+    line), the standard one (0x100000), and the automatic choice from the
+    codec's hint word (0: a unix16 batch flips it to the line policy for the
+    next launch, a mixed one back). Every launch bit-exact vs the oracle in
+    both modes: header-heavy and mixed batches at every record alignment,
+    records cut inside their first line (truncated headers), and the
+    lengths-driven decode."""
+    import torch
+    monkeypatch.setenv("ONC_RPC_VARIANT", str(variant))
+    codec = R.Codec(0)
+    try:
+        unix16 = S.call_unix16(1200, 40, seed=41)
+        mixed = S.mixed(1200, seed=42, pmin=0, pmax=300, exotic=0.2)
+        for hb in (unix16, unix16, mixed, mixed, unix16):
+            wire, off, st, _ = oracle.encode_batch(hb)
+            base = np.frombuffer(wire, np.uint8)
+            for shift in (0, 3, 8, 13):
+                w = np.concatenate([np.full(shift, 0xEE, np.uint8), base, np.zeros(16, np.uint8)])
+                o2 = off.astype(np.uint64) + np.uint64(shift)
+                for mode in (L.DECODE_SLICE, L.DECODE_BYTES):
+                    _same_decode(R.decode_host_wire(codec, w, o2, mode), oracle.decode_batch(w, o2, mode),
+                                 f"variant {variant:#x} shift {shift} mode {mode}")
+            # every record cut to a prefix (1..200 bytes): headers that end
+            # inside the first line, inside round 1, or past the window
+            rng = np.random.default_rng(variant + 1)
+            recs = []
+            for i in range(hb.n):
+                r = bytes(base[int(off[i]):int(off[i + 1])])
+                recs.append(r[:int(rng.integers(1, 200))] if i % 2 else r)
+            w2, o3 = L.records_from_wire(recs)
+            for mode in (L.DECODE_SLICE, L.DECODE_BYTES):
+                _same_decode(R.decode_host_wire(codec, w2, o3, mode), oracle.decode_batch(w2, o3, mode),
+                             f"variant {variant:#x} truncated mode {mode}")
+            # lengths-driven decode of the same wire
+            n = hb.n
+            lens = np.diff(off.astype(np.int64)).astype(np.uint32)
+            dw = torch.from_numpy(base.copy()).cuda()
+            rl = torch.from_numpy(lens.view(np.int32).copy()).cuda()
+            dec = R.DecodeBuffers(n)
+            ro = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+            codec.decode_lengths(dw, rl, n, 0, L.DECODE_SLICE, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1,
+                                 rec_off=ro)
+            codec.sync()
+            _same_decode(dec.to_host(), oracle.decode_batch(base, off.astype(np.uint64), L.DECODE_SLICE),
+                         f"variant {variant:#x} decode_lengths")
+    finally:
+        codec.close()
