@@ -37,6 +37,11 @@ struct onc_codec {
     const onc_msg* planned_msgs = nullptr;
     uint64_t planned_n = ~0ull;
     const int32_t* planned_status = nullptr;
+    // record lengths the plan wrote for the emit (the caller's rec_len or
+    // `lens`): set when the emit reads them (enc_args use_lens), else NULL
+    const uint32_t* planned_lens = nullptr;
+    uint32_t* lens = nullptr;      // codec-owned record lengths (per plan chunk)
+    uint64_t lens_cap = 0;
     uint32_t timing = 0;   // bitmask of ONC_K_* ids whose launches are bracketed
     struct Pending {
         int kernel;
@@ -104,6 +109,23 @@ void forget_plan(onc_codec* c) {
     c->planned_n = ~0ull;
     c->planned_msgs = nullptr;
     c->planned_status = nullptr;
+    c->planned_lens = nullptr;
+}
+
+int ensure_lens(onc_codec* c, uint64_t n) {
+    if (n <= c->lens_cap) return ONC_RC_OK;
+    uint64_t want = c->lens_cap ? c->lens_cap : 65536;
+    while (want < n) want *= 2;
+    if (c->lens) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(c->lens);
+        c->lens = nullptr;
+        c->lens_cap = 0;
+    }
+    if (hipMalloc(&c->lens, want * sizeof(uint32_t)) != hipSuccess) return ONC_RC_ENOMEM;
+    c->lens_cap = want;
+    forget_plan(c);
+    return ONC_RC_OK;
 }
 
 // scratch (u64 words): [tile_sum T | spare 2T | block_sum B | block_base B | 16]
@@ -208,6 +230,7 @@ int onc_codec_destroy(onc_codec* c) {
     for (auto e : c->spare) (void)hipEventDestroy(e);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->frame_scratch) (void)hipFree(c->frame_scratch);
+    if (c->lens) (void)hipFree(c->lens);
     if (c->dec_hint_host) (void)hipHostFree(c->dec_hint_host);
     delete c;
     return ONC_RC_OK;
@@ -404,6 +427,15 @@ int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
     return ONC_RC_OK;
 }
 
+// The wave-per-tile enc_emit reads the plan's record lengths instead of
+// planning again when the batch can hold AUTH_UNIX auths: its own plan would
+// load each credential's parameter block (ngids, name_len) one dependent
+// round trip after the descriptor (configs[0]-shaped batches). Variant bit
+// 0x20000 keeps the re-planning emit.
+bool use_lens(const onc_codec* c, const onc_batch* batch, const onc::EncArgs& a) {
+    return !a.ws && a.root == ONC_ROOT_RPC_MESSAGE && batch->unix_count != 0 && !(c->variant & 0x20000);
+}
+
 // enc_len: plans + per-tile and per-workgroup byte totals into the scratch.
 int enc_plan(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* rec_len,
              uint32_t root = ONC_ROOT_RPC_MESSAGE, uint64_t n_whole = 0) {
@@ -411,12 +443,19 @@ int enc_plan(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
     int rc = enc_args(c, batch, status, rec_len, a, root, n_whole);
     if (rc != ONC_RC_OK) return rc;
     forget_plan(c);
+    const bool lens = use_lens(c, batch, a);
+    if (lens && !a.rec_len) {
+        rc = ensure_lens(c, batch->n);
+        if (rc != ONC_RC_OK) return rc;
+        a.rec_len = c->lens;
+    }
     rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
     if (root == ONC_ROOT_RPC_MESSAGE) {
         c->planned_msgs = batch->msgs;
         c->planned_n = batch->n;
         c->planned_status = status;
+        c->planned_lens = lens ? a.rec_len : nullptr;
     }
     return ONC_RC_OK;
 }
@@ -437,6 +476,7 @@ int enc_emit(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_ca
     a.rec_off = rec_off;
     a.rec_len = nullptr;   // written by the plan
     a.base_dev = base_dev;
+    if (use_lens(c, batch, a)) a.len_in = c->planned_lens;
     if (!a.fused_base) {
         const uint64_t nblk = onc::num_len_blocks(batch->n);
         rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {

@@ -497,7 +497,8 @@ __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, 
     }
 }
 
-template <int kU, int kNT, bool kFused, bool kRoot = false, bool kGiven = false, bool kPre = false>
+template <int kU, int kNT, bool kFused, bool kRoot = false, bool kGiven = false, bool kPre = false,
+          bool kLen = false>
 __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile, uint64_t given = 0) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = tile * kEmitRecs;
@@ -510,6 +511,9 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     ONC_PROF(0);
     TileLoads<kFused> tl = tile_loads<kFused, kGiven>(a, tile, given);
     MsgRegs mr = issue_msg(a.msgs + r0 + min(lane, nrec - 1));
+    // kLen: the plan's length of the lane's record, issued with the rest
+    uint32_t glen = 0;
+    if constexpr (kLen) glen = a.len_in[r0 + min(lane, nrec - 1)];
     if constexpr (kFused) {
         static_assert(TileLoads<kFused>::kW == 16, "pin list below");
         asm volatile("" : "+v"(mr.q[0]), "+v"(mr.q[1]), "+v"(mr.q[2]), "+v"(mr.q[3]), "+v"(tl.v),
@@ -519,6 +523,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     } else {
         asm volatile("" : "+v"(mr.q[0]), "+v"(mr.q[1]), "+v"(mr.q[2]), "+v"(mr.q[3]), "+v"(tl.v), "+v"(tl.w[0]));
     }
+    if constexpr (kLen) asm volatile("" : "+v"(glen));
     const onc_msg dm = as_msg(mr);
     // output coordinates: byte 0 = the 16-aligned chunk base below the
     // caller's `out`, which sits at `origin` (any writer position)
@@ -533,10 +538,20 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     const uint64_t cred_ref = dm.cred.ref;
     if (lane < nrec) {
         const onc_msg& d = dm;
-        // the same function as enc_len: lengths agree
-        const RecPlan p = kRoot ? plan_root(d, a.unix, a.bounds, a.root) : plan_record(d, a.unix, a.bounds);
-        len = p.len;
-        hw = len ? meta_hw(p.meta) : 0;
+        if constexpr (kLen) {
+            // the plan's length (0: a failing record); the header is what is
+            // not payload (RpcMessage bodies: a Call's, an accepted Success's)
+            len = glen;
+            const bool body = d.msg_type == ONC_MSG_CALL ||
+                              (d.msg_type == ONC_MSG_REPLY && d.reply_stat == ONC_REPLY_ACCEPTED &&
+                               d.stat == ONC_ACCEPT_SUCCESS);
+            hw = len ? uint32_t((len - (body ? uint64_t(d.payload_len) : 0ull)) >> 2) : 0;
+        } else {
+            // the same function as enc_len: lengths agree
+            const RecPlan p = kRoot ? plan_root(d, a.unix, a.bounds, a.root) : plan_record(d, a.unix, a.bounds);
+            len = p.len;
+            hw = len ? meta_hw(p.meta) : 0;
+        }
         poff = d.payload_off;
         word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((payload + d.payload_off) & 3) == 0);
     }
@@ -1070,12 +1085,12 @@ __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
 // decode slower, 60 -> 69 us on c1: the dirty lines are written back at the
 // kernel boundary). Registers are left free (102 VGPRs, 4 waves per SIMD):
 // squeezed to 5 waves per SIMD every shape measured slower (spills).
-template <int kU, int kNT = 0, bool kFused = false, bool kRoot = false>
+template <int kU, int kNT = 0, bool kFused = false, bool kRoot = false, bool kLen = false>
 __global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) {
     __shared__ ImgTile s_tiles[kFastWaves];
     const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
     if (tile < num_emit_tiles(a.n))
-        enc_emit_tile<kU, kNT, kFused, kRoot, false, !kRoot>(a, s_tiles[threadIdx.x >> 6], tile);
+        enc_emit_tile<kU, kNT, kFused, kRoot, false, !kRoot, kLen>(a, s_tiles[threadIdx.x >> 6], tile);
 }
 
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
@@ -1108,12 +1123,14 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
                        dim3(64 * kFastWaves), 0, s, a);
         return hipGetLastError();
     }
-    if (a.fused_base)
-        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, true>), dim3(uint32_t(blocks)),
-                           dim3(64 * kFastWaves), 0, s, a);
-    else
-        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false>), dim3(uint32_t(blocks)),
-                           dim3(64 * kFastWaves), 0, s, a);
+    const dim3 g{uint32_t(blocks)}, b{uint32_t(64 * kFastWaves)};
+    if (a.len_in) {
+        if (a.fused_base) ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, true, false, true>), g, b, 0, s, a);
+        else ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false, false, true>), g, b, 0, s, a);
+        return hipGetLastError();
+    }
+    if (a.fused_base) ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, true>), g, b, 0, s, a);
+    else ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false>), g, b, 0, s, a);
     return hipGetLastError();
 }
 

@@ -57,6 +57,8 @@ struct EncArgs {
     uint32_t ws;            // enc_emit: the wave-specialised kernel (codec.hip enc_args decides)
     uint32_t root;          // ONC_ROOT_* (onc_encode_body); ONC_ROOT_RPC_MESSAGE for onc_encode
     const uint64_t* base_dev;   // optional: output bytes before this launch's first record (chunked encode)
+    const uint32_t* len_in;     // optional (wave-per-tile enc_emit): the plan's record lengths, read instead
+                                // of re-planning (no dependent AUTH_UNIX parameter load in the prologue)
 #ifdef ONC_EMIT_PROF
     uint64_t* prof;         // lab builds only (tools/emit_prof.hip): per-tile phase timestamps
 #endif

@@ -310,3 +310,45 @@ def test_decode_line_policy(R, oracle, monkeypatch, variant):
                          f"variant {variant:#x} decode_lengths")
     finally:
         codec.close()
+
+
+@pytest.mark.parametrize("variant", [0x400, 0x400 | 0x20000])
+@pytest.mark.parametrize("given_len", [False, True])
+def test_emit_from_plan_lengths(R, oracle, monkeypatch, variant, given_len):
+    """The wave-per-tile enc_emit reads the plan's record lengths (the
+    caller's rec_len, or the codec's own array) instead of planning again
+    when the batch has an AUTH_UNIX table (codec.hip use_lens; 0x20000 keeps
+    the re-planning emit): AUTH_UNIX-heavy and mixed batches with failing
+    records, through onc_encode and through onc_encode_plan + emit, and past
+    one 1M-record plan chunk — bytes, offsets and statuses equal to the
+    oracle's."""
+    import torch
+    monkeypatch.setenv("ONC_RPC_VARIANT", str(variant))
+    codec = R.Codec(0)
+    try:
+        for hb in (S.cpu_roundtrip(3000, seed=51), S.mixed(3000, seed=52, pmin=0, pmax=90, exotic=0.3),
+                   S.call_unix16(1_050_000, 20, seed=53)):
+            o_wire, o_off, o_st, o_len = oracle.encode_batch(hb)
+            db = R.DeviceBatch.from_host(hb)
+            n = hb.n
+            for plan_emit in (False, True):
+                if plan_emit and n > 1_000_000:
+                    continue          # plan + emit covers one plan (the chunked path is onc_encode's)
+                out = torch.zeros(len(o_wire) + 64, dtype=torch.uint8, device="cuda")
+                off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+                st = torch.empty(n, dtype=torch.int32, device="cuda")
+                rl = torch.empty(n, dtype=torch.int32, device="cuda") if given_len else None
+                if plan_emit:
+                    codec.encode_plan(db, st, rl)
+                    codec.encode_emit(db, out, off, st)
+                else:
+                    codec.encode(db, out, off, st, rl)
+                codec.sync()
+                what = f"variant {variant:#x} n {n} plan_emit {plan_emit}"
+                assert np.array_equal(st.cpu().numpy(), o_st), what
+                assert np.array_equal(off.cpu().numpy().view(np.uint64), o_off), what
+                if rl is not None:
+                    assert np.array_equal(rl.cpu().numpy().view(np.uint32), o_len), what
+                assert out.cpu().numpy()[:len(o_wire)].tobytes() == o_wire, what
+    finally:
+        codec.close()
