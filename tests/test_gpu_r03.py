@@ -1,7 +1,9 @@
 """GPU tests, round 3: the plan / emit contract (a plan is discarded by any
 call that reuses the handle's scratch; emit must get the plan's status
 array), and payloads at the first and last byte of a tightly sized payload
-arena on both enc_emit kernels. Bit-exact against the CPU oracle."""
+arena on both enc_emit kernels; the chunked encode at 2048-record chunks
+(message and body roots), the decode line policy and the emit from the
+plan's lengths. Bit-exact against the CPU oracle."""
 import numpy as np
 import pytest
 
@@ -350,5 +352,53 @@ def test_emit_from_plan_lengths(R, oracle, monkeypatch, variant, given_len):
                 if rl is not None:
                     assert np.array_equal(rl.cpu().numpy().view(np.uint32), o_len), what
                 assert out.cpu().numpy()[:len(o_wire)].tobytes() == o_wire, what
+    finally:
+        codec.close()
+
+
+@pytest.mark.parametrize("variant", [0, 0x200, 0x400])
+def test_small_encode_chunks(R, oracle, monkeypatch, variant):
+    """The chunked encode (codec.hip encode_batch) with 2048-record chunks
+    (ONC_RPC_ENC_CHUNK), so that small batches cross many chunk boundaries:
+    RpcMessage batches of every shape (mixed with failing records and odd
+    payloads, AUTH_UNIX-heavy with the plan's lengths read by the emit) at an
+    odd writer position with the capacity ending inside a later chunk, on the
+    automatic kernel choice and with each enc_emit kernel forced, and every
+    body root (onc_encode_body) — bytes, offsets, statuses and lengths equal
+    to the oracle's whole-batch loop."""
+    import torch
+    from test_body_roots import ROOTS, _valid_messages
+    monkeypatch.setenv("ONC_RPC_ENC_CHUNK", "2048")
+    monkeypatch.setenv("ONC_RPC_VARIANT", str(variant))
+    codec = R.Codec(0)
+    try:
+        for hb in (S.mixed(9001, seed=61, pmin=0, pmax=300, exotic=0.2), S.cpu_roundtrip(7000, seed=62),
+                   S.call_none(5000, 256, seed=63)):
+            for shift, cap_frac in ((0, None), (5, 0.7)):
+                o_wire, o_off, o_st, o_len = oracle.encode_batch(hb)
+                total = len(o_wire)
+                cap = total if cap_frac is None else int(total * cap_frac)
+                if cap != total:
+                    o_wire, o_off, o_st, o_len = oracle.encode_batch(hb, out_cap=cap)
+                db = R.DeviceBatch.from_host(hb)
+                buf = torch.full((shift + total + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+                off = torch.empty(hb.n + 1, dtype=torch.int64, device="cuda")
+                st = torch.empty(hb.n, dtype=torch.int32, device="cuda")
+                rl = torch.empty(hb.n, dtype=torch.int32, device="cuda")
+                codec.encode(db, buf[shift:], off, st, rl, out_cap=cap)
+                codec.sync()
+                what = f"variant {variant:#x} n {hb.n} shift {shift} cap {cap}"
+                b = buf.cpu().numpy()
+                assert np.array_equal(st.cpu().numpy(), o_st), what
+                assert np.array_equal(off.cpu().numpy().view(np.uint64), o_off), what
+                assert np.array_equal(rl.cpu().numpy().view(np.uint32), o_len), what
+                assert b[shift:shift + len(o_wire)].tobytes() == o_wire, what
+                assert (b[:shift] == 0xA5).all() and (b[shift + cap:] == 0xA5).all(), what
+        hb = L.build_batch(_valid_messages(5000, seed=64))
+        for root in ROOTS:
+            g = R.encode_body_host_batch(codec, root, hb)
+            o = oracle.encode_body_batch(root, hb)
+            assert np.array_equal(g[2], o[2]) and np.array_equal(g[3], o[3]), L.ROOT_NAMES[root]
+            assert np.array_equal(g[1], o[1]) and g[0] == o[0], L.ROOT_NAMES[root]
     finally:
         codec.close()
