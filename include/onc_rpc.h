@@ -399,8 +399,10 @@ int onc_encode(onc_codec* codec, const onc_batch* batch,
  * plan's statuses stand, emit only adds ONC_ENC_WRITE_ZERO), else
  * ONC_RC_EINVAL; any other call on the handle in between that uses its
  * scratch (every encode, decode_lengths and scan_lengths call) discards the
- * plan (then ONC_RC_EINVAL too). The descriptors must not change in between.
- * onc_encode = plan + emit. */
+ * plan (then ONC_RC_EINVAL too). The descriptors must not change in between,
+ * nor the plan's rec_len array when one was given (for a batch with an
+ * AUTH_UNIX table the emit reads the record lengths back from it instead of
+ * re-planning). onc_encode = plan + emit. */
 int onc_encode_plan(onc_codec* codec, const onc_batch* batch, int32_t* status, uint32_t* rec_len);
 int onc_encode_emit(onc_codec* codec, const onc_batch* batch, uint8_t* out, uint64_t out_cap,
                     uint64_t* rec_off, int32_t* status);
