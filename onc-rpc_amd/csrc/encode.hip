@@ -440,15 +440,56 @@ __device__ __forceinline__ void merge_chunk(const ChunkPlan& P, const uint32_t X
 // and kU stores (lanes past the last full chunk repeat it — same bytes to
 // the same address), and the next step is always issued (the surplus
 // after the last step re-reads the last chunk). The one or two partial
-// chunks at the span's edges are written after the loop, with byte stores
-// of only the span's bytes.
-template <int kU, int kNT, bool kByte>
+// chunks at the span's edges are written with byte stores of only the
+// span's bytes (EdgeChunks).
+//
+// The partial edge chunks of a span (lane 0: chunk 0 when the span starts
+// inside it; lane 1: chunk NCe - 1 when the span ends inside another chunk):
+// their payload loads are issued before the stream's first step, and they
+// are merged and stored once the first two steps are issued. Loaded after
+// the stream (as in round 2), the edge could not be waited for without
+// waiting for every store of the span (the in-order vmcnt): a full store
+// drain per span, on the wave that also starts the next span's staging (or,
+// in the wave-specialised kernel, on the consumer every other one then
+// waits for at the span's barrier).
+template <int kNT, bool kByte>
+struct EdgeChunks {
+    uint32_t X[4];           // only the loaded dwords stay live across the first steps' issue; the plan
+                             // (LDS reads) is taken again at the merge
+    __device__ __forceinline__ static bool mine(int32_t cf, int32_t cl, int32_t NCe, int lane) {
+        return (lane == 0 && cf == 1) || (lane == 1 && cl == NCe - 1 && (NCe - 1 > 0 || cf == 0));
+    }
+    __device__ __forceinline__ void issue(const ImgTile& T, uint32_t gsh, uint64_t B0, int32_t cf, int32_t cl,
+                                          int32_t NCe, int lane, uintptr_t dummy) {
+        if (mine(cf, cl, NCe, lane)) {
+            const ChunkPlan P = plan_chunk<kByte>(T, gsh, B0, lane == 0 ? 0 : NCe - 1, dummy);
+            load_chunk<kNT, kByte>(P, X);
+        }
+    }
+    __device__ __forceinline__ void finish(const EncArgs& a, const ImgTile& T, uint32_t gsh, uint64_t B0,
+                                           uint64_t S0, uint64_t E, int32_t cf, int32_t cl, int32_t NCe, int lane,
+                                           uintptr_t dummy) const {
+        if (mine(cf, cl, NCe, lane)) {
+            const int32_t c = lane == 0 ? 0 : NCe - 1;
+            const ChunkPlan P = plan_chunk<kByte>(T, gsh, B0, c, dummy);
+            const uint4 L = T.img[P.slot];
+            uint32_t v[4];
+            merge_chunk<kByte>(P, X, L, v);
+            const uint64_t o = B0 + (uint64_t(c) << 4);
+            store_chunk(a.out, o, max(o, S0), min(o + 16, E), v);
+        }
+    }
+};
+
+template <int kU, int kNT, bool kByte, bool kEarly = !kByte>
 __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, uint32_t gsh, uint64_t B0,
-                                            uint64_t S0, uint64_t E, int32_t NCe, uintptr_t dummy) {
+                                            uint64_t S0, uint64_t E1, int32_t NCe, uintptr_t dummy) {
     const int lane = threadIdx.x & 63;
     constexpr int32_t S = 64 * kU;
     const int32_t cf = S0 > B0 ? 1 : 0;                 // chunk 0 partial: span starts inside it
-    const int32_t cl = (E & 15) ? NCe - 1 : NCe;          // full chunks [cf, cl)
+    const int32_t cl = (E1 & 15) ? NCe - 1 : NCe;         // full chunks [cf, cl)
+    EdgeChunks<kNT, kByte> E;
+    if (kEarly) E.issue(T, gsh, B0, cf, cl, NCe, lane, dummy);
     if (cl > cf) {
         ChunkPlan Pa[kU], Pb[kU];
         uint32_t Xa[kU][4], Xb[kU][4];
@@ -469,31 +510,22 @@ __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, 
         else *d = u32x4{v[0], v[1], v[2], v[3]};                                          \
     }
         ONC_ISSUE(Pa, Xa, La, cf);
+        ONC_ISSUE(Pb, Xb, Lb, cf + S);
+        if (kEarly) E.finish(a, T, gsh, B0, S0, E1, cf, cl, NCe, lane, dummy);
         for (int32_t st = cf;; st += 2 * S) {
-            ONC_ISSUE(Pb, Xb, Lb, st + S);
             ONC_CONSUME(Pa, Xa, La, st);
             if (st + S >= cl) break;
             ONC_ISSUE(Pa, Xa, La, st + 2 * S);
             ONC_CONSUME(Pb, Xb, Lb, st + S);
             if (st + 2 * S >= cl) break;
+            ONC_ISSUE(Pb, Xb, Lb, st + 3 * S);
         }
 #undef ONC_ISSUE
 #undef ONC_CONSUME
     }
-    // partial edge chunks: lane 0 the first (if the span starts inside it),
-    // lane 1 the last (if the span ends inside it and it is another chunk)
-    const bool e0 = lane == 0 && cf == 1;
-    const bool e1 = lane == 1 && cl == NCe - 1 && (NCe - 1 > 0 || cf == 0);
-    if (e0 || e1) {
-        const int32_t c = e0 ? 0 : NCe - 1;
-        const ChunkPlan P = plan_chunk<kByte>(T, gsh, B0, c, dummy);
-        uint32_t X[4];
-        load_chunk<kNT, kByte>(P, X);
-        const uint4 L = T.img[P.slot];
-        uint32_t v[4];
-        merge_chunk<kByte>(P, X, L, v);
-        const uint64_t o = B0 + (uint64_t(c) << 4);
-        store_chunk(a.out, o, max(o, S0), min(o + 16, E), v);
+    if (!kEarly || cl <= cf) {
+        if (!kEarly) E.issue(T, gsh, B0, cf, cl, NCe, lane, dummy);
+        E.finish(a, T, gsh, B0, S0, E1, cf, cl, NCe, lane, dummy);
     }
 }
 
@@ -879,8 +911,8 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
 
 // stream_span for consumer `part` of `nparts`: the span's full chunks in
 // steps of 64 * kU chunks, this wave taking steps part, part + nparts, ...
-// (same two-register-set pipeline); part 0 also writes the partial edge
-// chunks.
+// (same two-register-set pipeline); part nparts - 1, which never has more
+// steps than another part, also writes the partial edge chunks.
 template <int kU, int kNT, bool kByte, int kInterior = 0>
 __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile& T, const SpanHdr& h, int part,
                                                  int nparts, uintptr_t dummy) {
@@ -892,6 +924,13 @@ __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile
     const int32_t cf = S0 > B0 ? 1 : 0;
     const int32_t cl = (E & 15) ? NCe - 1 : NCe;
     const int32_t nsteps = cl > cf ? (cl - cf + S - 1) / S : 0;
+    EdgeChunks<kNT, kByte> Ed;
+    const bool edge_part = part == nparts - 1;
+    // the edge loads issued before the first steps: 1 KiB steps (configs[3]
+    // enc_emit 440 -> 437 us); with 2 KiB steps the extra registers and the
+    // peeled loop cost more than the drain (configs[1] 106 -> 108-109 us)
+    constexpr bool kEarly = kU == 1;
+    if (kEarly && edge_part) Ed.issue(T, gsh, B0, cf, cl, NCe, lane, dummy);
     if (part < nsteps) {
         ChunkPlan Pa[kU], Pb[kU];
         uint32_t Xa[kU][4], Xb[kU][4];
@@ -917,34 +956,39 @@ __device__ __forceinline__ void stream_span_part(const EncArgs& a, const ImgTile
         else *d = u32x4{v[0], v[1], v[2], v[3]};                                          \
     }
         int32_t jj = part;
-        ONC_ISSUE(Pa, Xa, La, cf + S * jj);
-        for (;;) {
+        if constexpr (kEarly) {
+            ONC_ISSUE(Pa, Xa, La, cf + S * jj);
             ONC_ISSUE(Pb, Xb, Lb, cf + S * min(jj + nparts, nsteps - 1));
-            ONC_CONSUME(Pa, Xa, La, cf + S * jj);
-            jj += nparts;
-            if (jj >= nsteps) break;
-            ONC_ISSUE(Pa, Xa, La, cf + S * min(jj + nparts, nsteps - 1));
-            ONC_CONSUME(Pb, Xb, Lb, cf + S * jj);
-            jj += nparts;
-            if (jj >= nsteps) break;
+            if (edge_part) Ed.finish(a, T, gsh, B0, S0, E, cf, cl, NCe, lane, dummy);
+            for (;;) {
+                ONC_CONSUME(Pa, Xa, La, cf + S * jj);
+                jj += nparts;
+                if (jj >= nsteps) break;
+                ONC_ISSUE(Pa, Xa, La, cf + S * min(jj + nparts, nsteps - 1));
+                ONC_CONSUME(Pb, Xb, Lb, cf + S * jj);
+                jj += nparts;
+                if (jj >= nsteps) break;
+                ONC_ISSUE(Pb, Xb, Lb, cf + S * min(jj + nparts, nsteps - 1));
+            }
+        } else {
+            ONC_ISSUE(Pa, Xa, La, cf + S * jj);
+            for (;;) {
+                ONC_ISSUE(Pb, Xb, Lb, cf + S * min(jj + nparts, nsteps - 1));
+                ONC_CONSUME(Pa, Xa, La, cf + S * jj);
+                jj += nparts;
+                if (jj >= nsteps) break;
+                ONC_ISSUE(Pa, Xa, La, cf + S * min(jj + nparts, nsteps - 1));
+                ONC_CONSUME(Pb, Xb, Lb, cf + S * jj);
+                jj += nparts;
+                if (jj >= nsteps) break;
+            }
         }
 #undef ONC_ISSUE
 #undef ONC_CONSUME
     }
-    if (part == 0) {
-        const bool e0 = lane == 0 && cf == 1;
-        const bool e1 = lane == 1 && cl == NCe - 1 && (NCe - 1 > 0 || cf == 0);
-        if (e0 || e1) {
-            const int32_t c = e0 ? 0 : NCe - 1;
-            const ChunkPlan P = plan_chunk<kByte>(T, gsh, B0, c, dummy);
-            uint32_t X[4];
-            load_chunk<kNT, kByte>(P, X);
-            const uint4 L = T.img[P.slot];
-            uint32_t v[4];
-            merge_chunk<kByte>(P, X, L, v);
-            const uint64_t o = B0 + (uint64_t(c) << 4);
-            store_chunk(a.out, o, max(o, S0), min(o + 16, E), v);
-        }
+    if (edge_part && (!kEarly || part >= nsteps)) {
+        if (!kEarly) Ed.issue(T, gsh, B0, cf, cl, NCe, lane, dummy);
+        Ed.finish(a, T, gsh, B0, S0, E, cf, cl, NCe, lane, dummy);
     }
 }
 
