@@ -120,6 +120,24 @@ def test_capacity_and_invalid(codec, R, oracle):
     _check(R, codec, oracle, bad)
 
 
+@pytest.mark.parametrize("shift", [0, 4, 7, 12])
+def test_two_span_edges(codec, R, oracle, shift):
+    """configs[0]-shaped records (benches/bench.rs:86-101 + 64 B payload):
+    every 64-record tile streams as two spans on the word path, whose
+    partial edge chunks are loaded before the stream's first steps
+    (encode.hip EdgeChunks) — at writer positions that put the span edges
+    at every dword offset inside a chunk, and with the capacity ending
+    inside a tile's second span and inside a chunk."""
+    hb = S.cpu_roundtrip(20_000, seed=41)
+    _check(R, codec, oracle, hb, shift=shift)
+    total = len(oracle.encode_batch(hb)[0])
+    # record 64 * 157 + 50 lies in tile 157's second span; cut 3 bytes into its payload
+    rec = 64 * 157 + 50
+    cap = int(oracle.encode_batch(hb)[1][rec]) + 128 + 3
+    assert cap < total
+    _check(R, codec, oracle, hb, shift=shift, cap=cap)
+
+
 def test_maximal_auth_unix(codec, R, oracle):
     """Credential and verifier both AUTH_UNIX at the 200-byte limit (460-byte
     headers) with odd payloads: several spans per tile on the byte path."""
