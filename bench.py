@@ -86,6 +86,15 @@ def parse(argv=None):
     ap.add_argument("--no-pcie", action="store_true")
     ap.add_argument("--traffic-json", default=None,
                     help="per-kernel PMC traffic (default: the newest profiles/traffic_rNN[_<workload>].json)")
+    ap.add_argument("--cache", choices=["cold", "warm"], default="cold",
+                    help="c2: cold = every step decodes another of K identical wire copies, so the header lines a "
+                         "step reads were last touched >= 2x the 256 MiB Infinity Cache of other traffic ago; "
+                         "warm = the same wire every step")
+    ap.add_argument("--cache-leg", choices=["on", "off"], default="on",
+                    help="also measure the other cache state (c2: warm; c1: decode-only legs, warm and cold) and "
+                         "report it next to the primary line")
+    ap.add_argument("--variant", type=lambda s: int(s, 0), default=0,
+                    help="kernel variant bits (onc_codec_options.variant; A/B measurements only)")
     return ap.parse_args(argv)
 
 
@@ -343,7 +352,8 @@ def pcie_pipelined(args, torch, R, wl, hb, db, out, total_bytes, lens_np, rec_le
         msgs = hb.msgs
         pst = msgs["payload_off"].astype(np.int64)
         pen = pst + msgs["payload_len"].astype(np.int64)
-        kinds = [(msgs["cred_kind_len"] >> 24) == 3, (msgs["verf_kind_len"] >> 24) == 3]
+        import onc_rpc_amd.layout as L
+        kinds = [(msgs["cred_kind_len"] >> 24) == L.KIND_UNIX, (msgs["verf_kind_len"] >> 24) == L.KIND_UNIX]
         refs = [msgs["cred_ref"].astype(np.int64), msgs["verf_ref"].astype(np.int64)]
     for k, (lo, hi) in enumerate(bounds):
         nk = hi - lo
@@ -555,6 +565,40 @@ class Timing:
         torch.cuda.synchronize()
         self.ms_clean = ev2.elapsed_time(ev3)
         self.dom = R.K_NAMES[self.dom_id]
+        self.steps_n = steps
+
+
+MALL_BYTES = 256 * 2**20       # MI355X Infinity Cache (MI355X_MICROARCH.md chip table)
+
+
+def cold_copies(buf, touched_per_step):
+    """`buf` and identical clones of it, enough that a step rotating through
+    them reads lines last touched >= 2x the Infinity Cache of other steps'
+    reads ago (touched_per_step: bytes of lines one step reads; at least 3
+    copies)."""
+    k = 1 + max(2, -(-2 * MALL_BYTES // max(1, touched_per_step)))
+    return [buf] + [buf.clone() for _ in range(k - 1)]
+
+
+def rotating(copies):
+    """A callable returning the next of `copies` on every call."""
+    it = [0]
+
+    def nxt():
+        b = copies[it[0] % len(copies)]
+        it[0] += 1
+        return b
+    return nxt
+
+
+def dom_summary(tm, n, sum_W, sum_H, ms_per_step):
+    dom_ms, dom_cnt = tm.kstats[tm.dom]
+    us = dom_ms / dom_cnt * 1e3
+    alg = ALG_PER_LAUNCH[tm.dom](n, sum_W, sum_H) / max(1, round(tm.per_step.get(tm.dom, 1)))
+    return {"Mmsgs_per_s": n / (ms_per_step / 1e3) / 1e6, "ms_per_step": ms_per_step,
+            "ms_per_step_without_kernel_events": tm.ms_clean / tm.steps_n,
+            "kernel": tm.dom, "avg_launch_us": us, "achieved_GBs": alg / (us * 1e-6) / 1e9,
+            "frac": alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS}
 
 
 def load_traffic(path, wl, n, dom):
@@ -815,21 +859,35 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
     H = parsed_bytes(hb, lens_np)
     sum_W, sum_H = total_bytes, int(H.sum())
 
+    cache_note = ("loopback: the decode reads the wire this step's encode has just written (nontemporal stores); "
+                  "descriptors and payloads are re-read every step")
     if wl == "c2":
         codec.encode(db, out, rec_off, enc_status, rec_len)     # input wire (untimed)
         torch.cuda.synchronize()
         dec_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         frame_res = torch.zeros(5, dtype=torch.int64, device=dev)
+        # cold: a server decodes fresh socket bytes, so every step decodes
+        # another identical copy of the wire (the header lines it reads were
+        # last touched >= 2 x 256 MiB of other steps' reads ago); warm: the
+        # same wire every step (its header lines stay in the Infinity Cache)
+        copies = cold_copies(out, min(total_bytes, 128 * n)) if args.cache == "cold" else [out]
+        cache_note = (f"cold: the step decodes one of {len(copies)} identical wire copies in rotation (>= 2x the "
+                      f"256 MiB Infinity Cache of other reads between two reads of a line)" if len(copies) > 1 else
+                      "warm: the same wire every step (its header lines stay in the 256 MiB Infinity Cache)")
 
-        def step():
-            if args.frame:
-                codec.frame_stream(out, total_bytes, dec_off, n, frame_res)
-                codec.decode(out, dec_off, n, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1)
-            else:
-                # offsets from the lengths inside the decode (onc_decode_lengths);
-                # they are also written out (dec_off: the validation below)
-                codec.decode_lengths(out, rec_len, n, 0, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1,
-                                     rec_off=dec_off)
+        def make_step(nxt):
+            def step():
+                w = nxt()
+                if args.frame:
+                    codec.frame_stream(w, total_bytes, dec_off, n, frame_res)
+                    codec.decode(w, dec_off, n, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1)
+                else:
+                    # offsets from the lengths inside the decode (onc_decode_lengths);
+                    # they are also written out (dec_off: the validation below)
+                    codec.decode_lengths(w, rec_len, n, 0, mode, dec.msgs, dec.unix, dec.status, dec.aux0,
+                                         dec.aux1, rec_off=dec_off)
+            return step
+        step = make_step(rotating(copies))
     elif args.iov:
         # vectored encode; the contiguous encode of the same batch (untimed) is
         # the reference its headers and iovecs are checked against below
@@ -863,6 +921,35 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ms_max, ms_clean_max = float(t[0]), float(t[1])
+
+    # The other cache state, next to the primary line (SURVEY §7 "Cache
+    # effects"): c2 warm (or cold); for the loopbacks, the decode alone on the
+    # wire the last step encoded — the same buffer every step (warm) and
+    # rotating identical copies (cold, as a server decoding fresh bytes).
+    cache_legs = None
+    if args.cache_leg == "on" and not args.iov:
+        cache_legs = {}
+
+        def leg(stepfn):
+            tl = Timing(torch, R, codec, stepfn, args.steps, args.warmup, barrier)
+            return dom_summary(tl, n, sum_W, sum_H, tl.ms / args.steps)
+        if wl == "c2":
+            other = [out] if args.cache == "cold" else cold_copies(out, min(total_bytes, 128 * n))
+            key = "warm" if args.cache == "cold" else "cold"
+            cache_legs[key] = {**leg(make_step(rotating(other))), "copies": len(other)}
+            del other
+        else:
+            torch.cuda.synchronize()
+            cc = cold_copies(out, min(total_bytes, 128 * n))
+
+            def dec_step(nxt):
+                def s():
+                    codec.decode(nxt(), rec_off, n, mode, dec.msgs, dec.unix, dec.status, dec.aux0, dec.aux1)
+                return s
+            cache_legs["decode_only_warm"] = {**leg(dec_step(rotating([out]))), "copies": 1}
+            cache_legs["decode_only_cold"] = {**leg(dec_step(rotating(cc))), "copies": len(cc)}
+            del cc
+        torch.cuda.empty_cache()
 
     # Validation of the last step (device-side, size-independent checks).
     ok = True
@@ -963,7 +1050,9 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
         "config": {"workload": f"{desc}; {n} records per GPU ({args.mode} mode), HBM-resident",
                    "records_per_gpu": n, "wire_bytes_per_gpu": sum_W, "parsed_bytes_per_gpu": sum_H,
                    "decode_mode": args.mode,
+                   "cache": (args.cache if wl == "c2" else "loopback"), "cache_note": cache_note,
                    "parallelism": f"record-sharded x{world} (no collective)"},
+        "cache_legs": cache_legs,
         "wire_GiB_per_s": wire_gibs,
         "ms_per_step_without_kernel_events": ms_clean_max / steps,
         "step_alg_GBs": step_alg * world / (ms_per_step / 1e3) / 1e9,
@@ -1047,6 +1136,8 @@ def main():
     import onc_rpc_amd.shard as SH
     import onc_rpc_amd.synth as S
 
+    if args.variant:
+        R.DEFAULT_OPTIONS["variant"] = args.variant     # A/B measurements: every codec of the run
     dist = None
     torch.cuda.set_device(local_rank)
     if world > 1:

@@ -48,8 +48,12 @@ extern "C" {
  *    onc_encode_body_lengths); timing id 10 retired (ONC_K_FRAME_OFFSETS
  *    gone, the framer ids after it move down by one).
  * 5: decoded AUTH_UNIX slots compacted per 64-record group (onc_decoded):
- *    a slot's index is only what onc_auth.ref says, no longer 2i / 2i + 1. */
-#define ONC_RPC_ABI_VERSION 5
+ *    a slot's index is only what onc_auth.ref says, no longer 2i / 2i + 1.
+ * 6: onc_codec_create_ex + onc_codec_options (kernel choices, chunk sizes and
+ *    the decode policy are explicit options; the library reads no
+ *    environment variable), onc_codec_set_decode_policy, calls refuse to grow
+ *    scratch while the stream is being captured (ONC_RC_ECAPTURE). */
+#define ONC_RPC_ABI_VERSION 6
 
 /* ------------------------------------------------------------------------ */
 /* Wire discriminants (values are the on-wire u32s)                          */
@@ -190,6 +194,8 @@ extern "C" {
 #define ONC_RC_EHIP     -2
 #define ONC_RC_ENOMEM   -3
 #define ONC_RC_EALIGN   -4
+#define ONC_RC_ECAPTURE -5   /* the call would allocate scratch while its stream is being captured
+                                into a hipGraph: call onc_codec_reserve before the capture */
 
 /* ------------------------------------------------------------------------ */
 /* Descriptors                                                               */
@@ -307,15 +313,59 @@ typedef struct onc_decoded {
 
 typedef struct onc_codec onc_codec;
 
+/* Decode first-round policy (decode.hip): how much of each record's header
+ * the decode's first load round fetches. Results never depend on it, only
+ * the time. AUTO picks it per launch from the records the previous decode
+ * launch on the handle sampled (a word the kernel writes to mapped host
+ * memory, read at the next launch without a synchronisation); STANDARD
+ * fetches the first 44 bytes (short headers: AUTH_NONE calls, replies);
+ * LINE the rest of the record's first 128-byte line (long AUTH_UNIX
+ * headers). A hipGraph captures the policy in force when it is captured. */
+#define ONC_DECODE_POLICY_AUTO     0
+#define ONC_DECODE_POLICY_STANDARD 1
+#define ONC_DECODE_POLICY_LINE     2
+
+/* Kernel-variant bits (onc_codec_options.variant): measurement and test
+ * switches that force a kernel the codec would otherwise choose per batch.
+ * Results are bit-identical under every combination; production leaves 0. */
+#define ONC_VARIANT_EMIT_WS          0x200u    /* force the wave-specialised enc_emit */
+#define ONC_VARIANT_EMIT_TILE        0x400u    /* force the wave-per-tile enc_emit */
+#define ONC_VARIANT_WS_NO_INTERIOR   0x4000u   /* wave-specialised: no interior spans */
+#define ONC_VARIANT_WS_NO_FULL       0x8000u   /* wave-specialised: no full-interior spans */
+#define ONC_VARIANT_WS_PIPELINE      0x10000u  /* wave-specialised: the pipeline on header-heavy batches too */
+#define ONC_VARIANT_EMIT_REPLAN      0x20000u  /* wave-per-tile enc_emit re-plans instead of reading the plan's lengths */
+#define ONC_VARIANT_WHOLE_PLAN       0x40000u  /* plan a large batch whole instead of in chunks */
+
+#define ONC_OPT_FORCE_SCAN 0x1u   /* always launch the separate block-scan kernels (tests of that path) */
+
+/* Options of onc_codec_create_ex; all-zero (or a NULL pointer) = the
+ * defaults, which are what onc_codec_create uses. The library reads nothing
+ * from the environment. */
+typedef struct onc_codec_options {
+    uint32_t size;           /* sizeof(onc_codec_options), or 0 */
+    uint32_t flags;          /* ONC_OPT_* */
+    int32_t  decode_policy;  /* ONC_DECODE_POLICY_* */
+    uint32_t variant;        /* ONC_VARIANT_* bits (A/B measurements and tests; 0 in production) */
+    uint64_t enc_chunk;      /* records per plan + emit chunk of a large encode (rounded down to a
+                                multiple of 1024; 0 = 1M) */
+    uint64_t frame_chunk;    /* bytes per onc_frame_stream chunk (>= 64; 0 = 64 KiB) */
+} onc_codec_options;
+
 /* One handle per device: a HIP stream + scan scratch. `hip_stream` may be
  * NULL (the device's null stream) or a hipStream_t owned by the caller. */
 int onc_codec_create(onc_codec** out, int device, void* hip_stream);
+int onc_codec_create_ex(onc_codec** out, int device, void* hip_stream, const onc_codec_options* options);
 int onc_codec_destroy(onc_codec* codec);
 int onc_codec_set_stream(onc_codec* codec, void* hip_stream);
+int onc_codec_set_decode_policy(onc_codec* codec, int policy);
 int onc_codec_sync(onc_codec* codec);
-/* Pre-size the scan scratch for batches of up to max_records, so that later
- * calls perform no allocation (required before capturing calls into a
- * hipGraph; otherwise scratch grows on demand with a synchronous hipMalloc). */
+/* Pre-size the scratch for batches of up to max_records (scan totals, the
+ * plan's record lengths), so that later encode / decode / scan calls of up
+ * to that many records perform no allocation. Required before capturing
+ * calls into a hipGraph: a call that would grow the scratch while its
+ * stream is capturing returns ONC_RC_ECAPTURE (outside a capture the
+ * scratch grows on demand with a synchronous hipMalloc). onc_frame_stream
+ * keeps its own per-chunk scratch, sized by its first call. */
 int onc_codec_reserve(onc_codec* codec, uint64_t max_records);
 /* Last HIP error string seen by this handle ("" if none). */
 const char* onc_codec_last_error(const onc_codec* codec);
@@ -472,9 +522,9 @@ int32_t onc_expected_message_len(const uint8_t* data, uint64_t len, uint32_t* ou
  *                     ONC_ERR_INCOMPLETE_MESSAGE {aux0 = bytes left,
  *                     aux1 = record length} (wait for more data).
  * The stream is cut into 64 KiB chunks framed speculatively in parallel and
- * verified (frame.hip); ONC_RPC_FRAME_CHUNK (bytes, >= 64) in the
- * environment at onc_codec_create overrides the chunk size (tests use small
- * chunks to exercise the multi-chunk logic). SURVEY §8(f) rank 1. */
+ * verified (frame.hip); onc_codec_options.frame_chunk overrides the chunk
+ * size (tests use small chunks to exercise the multi-chunk logic).
+ * SURVEY §8(f) rank 1. */
 int onc_frame_stream(onc_codec* codec, const uint8_t* wire, uint64_t len,
                      uint64_t* rec_off, uint64_t max_records, uint64_t* result);
 

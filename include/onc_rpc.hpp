@@ -499,6 +499,15 @@ public:
     const ReplyBody* reply_body() const { return message_.reply_body(); }
     bool operator==(const RpcMessage& o) const { return xid_ == o.xid_ && message_ == o.message_; }
 
+    // Single-message calls: each is a whole GPU round trip (the message's
+    // descriptor and arenas copied to the device, the kernels, the results
+    // copied back, a stream synchronisation) — tens of microseconds where the
+    // reference's CPU call takes ~100 ns (tests/cpp/test_mirror.cpp
+    // test_single_message_cost prints both). They exist for tests and tiny
+    // batches; a caller with many messages uses BatchEncoder / BatchDecoder
+    // (one launch per batch). The same holds for every body type's
+    // serialised_len / serialise_into / try_from taking a Codec.
+    //
     // serialised_len (rpc_message.rs:201-204), computed by the encoder's
     // length kernel. Throws std::logic_error where the reference panics.
     uint32_t serialised_len(Codec& codec) const;

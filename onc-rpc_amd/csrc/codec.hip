@@ -27,10 +27,12 @@ struct onc_codec {
     uint32_t* dec_hint_host = nullptr;
     uint32_t* dec_hint_dev = nullptr;
     uint64_t frame_chunks = 0;
-    uint64_t frame_chunk = onc::kFrameChunkDefault;   // ONC_RPC_FRAME_CHUNK at create (bytes, >= 64)
-    uint64_t enc_chunk = 0;    // ONC_RPC_ENC_CHUNK at create (records, multiple of 1024; 0 = kEncChunk)
-    bool force_scan = false;   // ONC_RPC_FORCE_SCAN=1 at create: always launch the block scan (tests)
-    uint32_t variant = 0;      // ONC_RPC_VARIANT at create: kernel variant bits (A/B measurements)
+    // onc_codec_options (onc_codec_create_ex); nothing is read from the environment
+    uint64_t frame_chunk = onc::kFrameChunkDefault;   // bytes per framing chunk (>= 64)
+    uint64_t enc_chunk = 0;    // records per plan + emit chunk (multiple of 1024; 0 = kEncChunk)
+    bool force_scan = false;   // ONC_OPT_FORCE_SCAN: always launch the block scan (tests)
+    uint32_t variant = 0;      // ONC_VARIANT_* bits (A/B measurements, tests)
+    int decode_policy = ONC_DECODE_POLICY_AUTO;
     // the batch whose plan (onc_encode_plan) the scratch holds, and the
     // status array that plan filled; every other call that writes the
     // scratch discards it (forget_plan)
@@ -79,11 +81,19 @@ hipEvent_t take_event(onc_codec* c) {
     return e;
 }
 
-// Launch one kernel, bracketed by events when timing is on.
+// The handle's stream is being captured into a hipGraph: nothing may
+// allocate, synchronise or time launches with events on it then.
+bool capturing(const onc_codec* c) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(c->stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+// Launch one kernel, bracketed by events when timing is on (never inside a
+// capture).
 template <class F>
 int run(onc_codec* c, int kernel, const char* what, F&& launch) {
     hipEvent_t a = nullptr, b = nullptr;
-    const bool timed = (c->timing >> kernel) & 1u;
+    const bool timed = ((c->timing >> kernel) & 1u) && !capturing(c);
     if (timed) {
         a = take_event(c);
         b = take_event(c);
@@ -112,8 +122,14 @@ void forget_plan(onc_codec* c) {
     c->planned_lens = nullptr;
 }
 
+int refuse_in_capture(onc_codec* c) {
+    c->last_error = "scratch would grow during a stream capture: call onc_codec_reserve first";
+    return ONC_RC_ECAPTURE;
+}
+
 int ensure_lens(onc_codec* c, uint64_t n) {
     if (n <= c->lens_cap) return ONC_RC_OK;
+    if (capturing(c)) return refuse_in_capture(c);
     uint64_t want = c->lens_cap ? c->lens_cap : 65536;
     while (want < n) want *= 2;
     if (c->lens) {
@@ -133,6 +149,7 @@ uint64_t scratch_words(uint64_t T) { return 3 * T + 2 * (T / 4 + 1) + 16; }
 
 int ensure_scratch(onc_codec* c, uint64_t tiles) {
     if (tiles <= c->scratch_tiles) return ONC_RC_OK;
+    if (capturing(c)) return refuse_in_capture(c);
     uint64_t want = c->scratch_tiles ? c->scratch_tiles : 1024;
     while (want < tiles) want *= 2;
     if (c->scratch) {
@@ -167,15 +184,18 @@ int set_device(onc_codec* c) {
     return ONC_RC_OK;
 }
 
-// The message decode's first-round policy from the previous launch's sample
-// (a plain read of mapped host memory: no synchronisation, at worst one
-// launch stale); variant bits 0x80000 / 0x100000 force it.
-void set_decode_policy(onc_codec* c, onc::DecArgs& a) {
+// The message decode's first-round policy: pinned (ONC_DECODE_POLICY_LINE /
+// _STANDARD), or (AUTO) from the previous launch's sample — a plain read of
+// mapped host memory: no synchronisation, at worst one launch stale. A
+// capture records the kernel instance of the policy in force.
+void decode_policy(onc_codec* c, onc::DecArgs& a) {
     a.hint = c->dec_hint_dev;
-    const uint32_t seen = *reinterpret_cast<volatile uint32_t*>(c->dec_hint_host);
-    a.line = seen >= onc::kLine1Min ? 1u : 0u;
-    if (c->variant & 0x80000) a.line = 1;
-    if (c->variant & 0x100000) a.line = 0;
+    if (c->decode_policy == ONC_DECODE_POLICY_AUTO) {
+        const uint32_t seen = *reinterpret_cast<volatile uint32_t*>(c->dec_hint_host);
+        a.line = seen >= onc::kLine1Min ? 1u : 0u;
+    } else {
+        a.line = c->decode_policy == ONC_DECODE_POLICY_LINE ? 1u : 0u;
+    }
 }
 
 }  // namespace
@@ -185,23 +205,27 @@ extern "C" {
 int onc_abi_version(void) { return ONC_RPC_ABI_VERSION; }
 
 int onc_codec_create(onc_codec** out, int device, void* hip_stream) {
+    return onc_codec_create_ex(out, device, hip_stream, nullptr);
+}
+
+int onc_codec_create_ex(onc_codec** out, int device, void* hip_stream, const onc_codec_options* o) {
     if (!out) return ONC_RC_EINVAL;
     *out = nullptr;
+    if (o && o->size != 0 && o->size < sizeof(onc_codec_options)) return ONC_RC_EINVAL;
+    if (o && (o->decode_policy < ONC_DECODE_POLICY_AUTO || o->decode_policy > ONC_DECODE_POLICY_LINE ||
+              (o->frame_chunk != 0 && o->frame_chunk < 64) || (o->flags & ~ONC_OPT_FORCE_SCAN) != 0))
+        return ONC_RC_EINVAL;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return ONC_RC_EINVAL;
     onc_codec* c = new onc_codec();
     c->device = device;
     c->stream = static_cast<hipStream_t>(hip_stream);
-    const char* fs = getenv("ONC_RPC_FORCE_SCAN");
-    c->force_scan = fs && fs[0] == '1';
-    const char* vv = getenv("ONC_RPC_VARIANT");
-    if (vv) c->variant = uint32_t(strtoul(vv, nullptr, 0));
-    const char* ec = getenv("ONC_RPC_ENC_CHUNK");
-    if (ec) c->enc_chunk = strtoull(ec, nullptr, 10) / onc::kLenRecs * onc::kLenRecs;
-    const char* fc = getenv("ONC_RPC_FRAME_CHUNK");
-    if (fc) {
-        const unsigned long long v = strtoull(fc, nullptr, 10);
-        if (v >= 64) c->frame_chunk = v;
+    if (o) {
+        c->force_scan = (o->flags & ONC_OPT_FORCE_SCAN) != 0;
+        c->variant = o->variant;
+        c->decode_policy = o->decode_policy;
+        c->enc_chunk = o->enc_chunk / onc::kLenRecs * onc::kLenRecs;
+        if (o->frame_chunk) c->frame_chunk = o->frame_chunk;
     }
     if (set_device(c) != ONC_RC_OK) {
         delete c;
@@ -242,6 +266,12 @@ int onc_codec_set_stream(onc_codec* c, void* hip_stream) {
     return ONC_RC_OK;
 }
 
+int onc_codec_set_decode_policy(onc_codec* c, int policy) {
+    if (!c || policy < ONC_DECODE_POLICY_AUTO || policy > ONC_DECODE_POLICY_LINE) return ONC_RC_EINVAL;
+    c->decode_policy = policy;
+    return ONC_RC_OK;
+}
+
 int onc_codec_sync(onc_codec* c) {
     if (!c) return ONC_RC_EINVAL;
     if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
@@ -253,7 +283,10 @@ int onc_codec_sync(onc_codec* c) {
 int onc_codec_reserve(onc_codec* c, uint64_t max_records) {
     if (!c) return ONC_RC_EINVAL;
     if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
-    return ensure_scratch(c, onc::num_emit_tiles(max_records));
+    const int rc = ensure_scratch(c, onc::num_emit_tiles(max_records));
+    if (rc != ONC_RC_OK) return rc;
+    // the plan's record lengths (an encode's chunk at most)
+    return ensure_lens(c, std::min(max_records, c->enc_chunk ? c->enc_chunk : onc::kFusedBlocks * onc::kLenRecs));
 }
 
 const char* onc_codec_last_error(const onc_codec* c) { return c ? c->last_error.c_str() : "null codec"; }
@@ -416,7 +449,7 @@ int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
     // same with 1 KiB steps (long payloads: configs[3] 1770 vs 1815 us)
     const bool big = batch->payload_len >= 512 * nw;
     const bool ws_shape = batch->payload_len >= 128 * nw && (onc::num_emit_tiles(n) <= kWsMaxTiles || big);
-    a.ws = ((c->variant & 0x200) || (!(c->variant & 0x400) && n && ws_shape)) ? (big ? 2u : 1u) : 0u;
+    a.ws = ((c->variant & ONC_VARIANT_EMIT_WS) || (!(c->variant & ONC_VARIANT_EMIT_TILE) && n && ws_shape)) ? (big ? 2u : 1u) : 0u;
     a.root = root;
     if (root != ONC_ROOT_RPC_MESSAGE) a.ws = 0;   // body roots: the wave-per-tile kernel
     // the wave-specialised kernel checks the real payload volume itself
@@ -433,7 +466,7 @@ int enc_args(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
 // round trip after the descriptor (configs[0]-shaped batches). Variant bit
 // 0x20000 keeps the re-planning emit.
 bool use_lens(const onc_codec* c, const onc_batch* batch, const onc::EncArgs& a) {
-    return !a.ws && a.root == ONC_ROOT_RPC_MESSAGE && batch->unix_count != 0 && !(c->variant & 0x20000);
+    return !a.ws && a.root == ONC_ROOT_RPC_MESSAGE && batch->unix_count != 0 && !(c->variant & ONC_VARIANT_EMIT_REPLAN);
 }
 
 // enc_len: plans + per-tile and per-workgroup byte totals into the scratch.
@@ -443,11 +476,17 @@ int enc_plan(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
     int rc = enc_args(c, batch, status, rec_len, a, root, n_whole);
     if (rc != ONC_RC_OK) return rc;
     forget_plan(c);
+    // the lengths the emit reads back live in codec-owned memory (the
+    // caller's rec_len, when given, receives a copy): nothing the caller
+    // does between plan and emit can make the emit's placement disagree
+    // with the plan's totals
+    // declared AUTH_UNIX lengths planned as given; the emit checks the blocks
+    a.decl = root == ONC_ROOT_RPC_MESSAGE ? 1u : 0u;
     const bool lens = use_lens(c, batch, a);
-    if (lens && !a.rec_len) {
+    if (lens) {
         rc = ensure_lens(c, batch->n);
         if (rc != ONC_RC_OK) return rc;
-        a.rec_len = c->lens;
+        a.len_out = c->lens;
     }
     rc = run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });
     if (rc != ONC_RC_OK) return rc;
@@ -455,7 +494,7 @@ int enc_plan(onc_codec* c, const onc_batch* batch, int32_t* status, uint32_t* re
         c->planned_msgs = batch->msgs;
         c->planned_n = batch->n;
         c->planned_status = status;
-        c->planned_lens = lens ? a.rec_len : nullptr;
+        c->planned_lens = lens ? c->lens : nullptr;
     }
     return ONC_RC_OK;
 }
@@ -480,7 +519,9 @@ int enc_emit(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_ca
     if (!a.fused_base) {
         const uint64_t nblk = onc::num_len_blocks(batch->n);
         rc = run(c, ONC_K_SCAN_TILES, "scan", [&] {
-            return onc::launch_scan_tiles(a.block_sum, a.block_base, nblk, 0, rec_off + batch->n, c->stream);
+            // (no total out: the emit's last record writes rec_off[n], and in a
+            // chunked encode rec_off[n] is the next chunk's base)
+            return onc::launch_scan_tiles(a.block_sum, a.block_base, nblk, 0, nullptr, c->stream);
         });
         if (rc != ONC_RC_OK) return rc;
     }
@@ -501,7 +542,7 @@ int encode_batch(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t ou
                  int32_t* status, uint32_t* rec_len, uint32_t root) {
     const uint64_t n = batch->n;
     const uint64_t chunk = c->enc_chunk ? c->enc_chunk : kEncChunk;
-    if (n <= chunk || (c->variant & 0x40000)) {     // 0x40000: whole-batch plan (lab)
+    if (n <= chunk || (c->variant & ONC_VARIANT_WHOLE_PLAN)) {     // whole-batch plan (lab)
         const int rc = enc_plan(c, batch, status, rec_len, root);
         if (rc != ONC_RC_OK) return rc;
         return enc_emit(c, batch, out, out_cap, rec_off, status, nullptr, root);
@@ -712,7 +753,7 @@ int onc_decode(onc_codec* c, const uint8_t* wire, const uint64_t* rec_off, uint6
     a.rec_off = rec_off;
     a.out = *out;
     a.variant = c->variant;
-    set_decode_policy(c, a);
+    decode_policy(c, a);
     return run(c, ONC_K_DEC_PARSE, "decode", [&] { return onc::launch_decode(a, mode, c->stream); });
 }
 
@@ -735,7 +776,7 @@ int onc_decode_lengths(onc_codec* c, const uint8_t* wire, const uint32_t* rec_le
     a.wire = wire;
     a.out = *out;
     a.variant = c->variant;
-    set_decode_policy(c, a);
+    decode_policy(c, a);
     a.rec_len = rec_len;
     a.tile_sum = c->scratch;
     a.blk_sum = c->scratch + 3 * T;
@@ -761,9 +802,8 @@ int onc_scan_lengths(onc_codec* c, const uint32_t* rec_len, uint64_t n, uint64_t
     if (!c || !rec_off || (n && !rec_len)) return ONC_RC_EINVAL;
     if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
     if (n == 0) {
-        const hipError_t e = hipMemcpyAsync(rec_off, &base, sizeof(base), hipMemcpyHostToDevice, c->stream);
-        if (e != hipSuccess) return fail(c, e, "hipMemcpyAsync");
-        return onc_codec_sync(c);   // `base` lives on this stack frame
+        const hipError_t e = onc::launch_store_u64(rec_off, base, c->stream);
+        return e == hipSuccess ? ONC_RC_OK : fail(c, e, "store_u64");
     }
     const uint64_t tiles = onc::num_tiles(n);
     int rc = ensure_scratch(c, tiles);

@@ -132,6 +132,21 @@ __device__ __forceinline__ bool in_arena(uint64_t off, uint64_t len, uint64_t si
     return off <= size && len <= size - off;
 }
 
+// AuthUnixParams::serialised_len (unix_params.rs:219-230) of a name length and gid count
+__host__ __device__ __forceinline__ uint32_t unix_body_len(uint32_t nl, uint32_t ng) { return 20u + 4u * words4(nl) + 4u * ng; }
+// A declared AUTH_UNIX length (onc_auth.len, ABI 6) that some parameter block can have: a multiple of 4
+// between the empty block (20) and a 255-byte name with 16 gids.
+__host__ __device__ __forceinline__ bool unix_len_plausible(uint32_t l) {
+    return l >= 20u && (l & 3u) == 0 && l <= unix_body_len(ONC_MAX_MACHINE_NAME_LEN, ONC_MAX_GIDS);
+}
+
+// kDecl: an AUTH_UNIX auth that declares its length (onc_auth.len != 0) is
+// planned from the descriptor alone — no parameter-block load; the block's
+// checks (the name / gid panics, the name's arena bounds, declared ==
+// serialised length) are deferred to the emit (check_declared_unix). The
+// encoder's length pass runs this form first and the full one only for a
+// record it fails (include/onc_rpc.h onc_auth).
+template <bool kDecl = false>
 __device__ __forceinline__ AuthPlan plan_auth(const onc_auth& a, const onc_unix_params* unix, const Bounds& bd) {
     AuthPlan p;
     const uint32_t kind = a.kind_len >> 24;
@@ -139,6 +154,14 @@ __device__ __forceinline__ AuthPlan plan_auth(const onc_auth& a, const onc_unix_
     p.status = ONC_OK;
     if (kind == ONC_KIND_UNIX) {
         if (a.ref >= bd.n_unix) { p.status = ONC_ENC_BAD_DESCRIPTOR; p.words = 0; p.assoc = 0; return p; }
+        if (kDecl && len != 0) {
+            if (!unix_len_plausible(len)) { p.status = ONC_ENC_BAD_DESCRIPTOR; p.words = 0; p.assoc = 0; return p; }
+            p.words = 2 + len / 4;
+            // associated_data_len = len - 8 - pad(name) in [len - 11, len - 8]: with len a multiple
+            // of 4, len - 8 > 200 exactly when the true value is
+            p.assoc = len - 8;
+            return p;
+        }
         const onc_unix_params* u = unix + a.ref;
         const uint32_t nl = u->name_len, ng = u->ngids;
         // AuthUnixParams::new panics (unix_params.rs:149), then Gids (:47)
@@ -147,6 +170,8 @@ __device__ __forceinline__ AuthPlan plan_auth(const onc_auth& a, const onc_unix_
         if (nl != 0 && !in_arena(u->name_off, nl, bd.auth_len)) {
             p.status = ONC_ENC_BAD_DESCRIPTOR; p.words = 0; p.assoc = 0; return p;
         }
+        // a declared length must be the block's
+        if (len != 0 && len != unix_body_len(nl, ng)) { p.status = ONC_ENC_BAD_DESCRIPTOR; p.words = 0; p.assoc = 0; return p; }
         // id + len + stamp + opaque(name) + uid + gid + ngids + gids
         p.words = 2 + 1 + 1 + words4(nl) + 3 + ng;
         p.assoc = 12 + nl + 4 * ng;               // unix_params.rs:234-245
@@ -177,6 +202,9 @@ __device__ __forceinline__ uint32_t meta_hw(uint32_t m) { return m >> 16; }
 // serialise_into in reference order: descriptor / construction panics
 // (cred, then verf), oversize (rpc_message.rs:146-151), then the
 // associated-data assert (flavor.rs:110, cred before verf).
+// kDecl: declared AUTH_UNIX lengths are taken as given (plan_auth); a record
+// that fails this form fails the full one too, with the full one's status.
+template <bool kDecl = false>
 __device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_params* unix, const Bounds& bd) {
     RecPlan r;
     r.len = 0;
@@ -186,9 +214,9 @@ __device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_
     uint64_t body = 0;
     uint32_t assoc_c = 0, assoc_v = 0;
     if (d.msg_type == ONC_MSG_CALL) {
-        AuthPlan c = plan_auth(d.cred, unix, bd);
+        AuthPlan c = plan_auth<kDecl>(d.cred, unix, bd);
         if (c.status) { r.status = c.status; return r; }
-        AuthPlan v = plan_auth(d.verf, unix, bd);
+        AuthPlan v = plan_auth<kDecl>(d.verf, unix, bd);
         if (v.status) { r.status = v.status; return r; }
         cw = c.words; vw = v.words;
         assoc_c = c.assoc; assoc_v = v.assoc;
@@ -197,7 +225,7 @@ __device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_
     } else if (d.msg_type == ONC_MSG_REPLY) {
         if (d.reply_stat == ONC_REPLY_ACCEPTED) {
             if (d.stat > ONC_ACCEPT_SYSTEM_ERR) { r.status = ONC_ENC_BAD_DESCRIPTOR; return r; }
-            AuthPlan v = plan_auth(d.verf, unix, bd);
+            AuthPlan v = plan_auth<kDecl>(d.verf, unix, bd);
             if (v.status) { r.status = v.status; return r; }
             vw = v.words; assoc_v = v.assoc;
             // mark, xid, mtype, reply_stat, verf, accept_stat [, low, high]
@@ -224,6 +252,28 @@ __device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_
     r.meta = cw | (vw << 8) | (hw << 16);
     return r;
 }
+
+// The checks plan_auth<true> deferred, in plan_auth's order, on the first 32
+// bytes of the auth's parameter block (q0 = stamp, uid, gid, ngids; q1 =
+// name_off, name_len, reserved).
+__device__ __forceinline__ int32_t check_declared_unix(const u32x4& q0, const u32x4& q1, uint32_t declared,
+                                                       uint64_t auth_len) {
+    const uint32_t ng = q0.w, nl = q1.z;
+    const uint64_t noff = uint64_t(q1.x) | (uint64_t(q1.y) << 32);
+    if (nl > ONC_MAX_MACHINE_NAME_LEN) return ONC_ENC_NAME_GT_255;
+    if (ng > ONC_MAX_GIDS) return ONC_ENC_GIDS_GT_16;
+    if (nl != 0 && !in_arena(noff, nl, auth_len)) return ONC_ENC_BAD_DESCRIPTOR;
+    if (unix_body_len(nl, ng) != declared) return ONC_ENC_BAD_DESCRIPTOR;
+    return ONC_OK;
+}
+
+// The emit's side of plan_record<true>: the first failing deferred check of
+// a record's declared AUTH_UNIX auths (credential before verifier), run by
+// put_unix_words on the block words it loads anyway.
+struct DeclCheck {
+    uint64_t auth_len;   // the auth arena's size (the machine name's bounds)
+    int32_t st;
+};
 
 struct EncSrc {
     const onc_unix_params* unix;
@@ -278,8 +328,16 @@ __device__ __forceinline__ UnixRegs issue_unix(const onc_unix_params* unix, uint
 // parameter block, preceded (kLen) by its serialised_len — the opaque length
 // AuthFlavor::serialise_into writes before it (flavor.rs:123-126).
 template <bool kLen, class Sink>
-__device__ __forceinline__ void put_unix_words(const UnixRegs& u, const EncSrc& s, Sink& out) {
+__device__ __forceinline__ void put_unix_words(const UnixRegs& u, const EncSrc& s, Sink& out,
+                                               DeclCheck* dc = nullptr, uint32_t declared = 0) {
     const u32x4* q = u.q;
+    if (dc && declared != 0) {
+        // a block that fails is not serialised: the record stops here, never
+        // past the declared extent its placement has (nothing written so far
+        // exceeds it)
+        if (dc->st == ONC_OK) dc->st = check_declared_unix(q[0], q[1], declared, dc->auth_len);
+        if (dc->st != ONC_OK) return;
+    }
     const uint32_t stamp = q[0].x, uid = q[0].y, gid = q[0].z, ng = q[0].w;
     const uint64_t name_off = uint64_t(q[1].x) | (uint64_t(q[1].y) << 32);
     const uint32_t nl = q[1].z;
@@ -300,8 +358,9 @@ __device__ __forceinline__ void put_unix_words(const UnixRegs& u, const EncSrc& 
 
 // ... of unix-table entry `ref`
 template <bool kLen, class Sink>
-__device__ __forceinline__ void put_unix_words(uint64_t ref, const EncSrc& s, Sink& out) {
-    put_unix_words<kLen>(issue_unix(s.unix, ref), s, out);
+__device__ __forceinline__ void put_unix_words(uint64_t ref, const EncSrc& s, Sink& out, DeclCheck* dc = nullptr,
+                                               uint32_t declared = 0) {
+    put_unix_words<kLen>(issue_unix(s.unix, ref), s, out, dc, declared);
 }
 
 // Opaque::serialise_into (opaque.rs:38-56) of an auth body: length, body
@@ -319,27 +378,31 @@ __device__ __forceinline__ void put_opaque_words(const onc_auth& a, const EncSrc
 // whose block the caller issued with its other loads)
 template <class Sink>
 __device__ __forceinline__ void put_auth_words(const onc_auth& a, const EncSrc& s, Sink& out,
-                                               const UnixRegs* pre = nullptr, bool use_pre = false) {
+                                               const UnixRegs* pre = nullptr, bool use_pre = false,
+                                               DeclCheck* dc = nullptr) {
     const uint32_t kind = a.kind_len >> 24;
     out(bswap(kind == ONC_KIND_UNKNOWN ? a.id : kind));
     if (kind != ONC_KIND_UNIX) {
         put_opaque_words(a, s, out);
         return;
     }
-    if (use_pre) put_unix_words<true>(*pre, s, out);
-    else put_unix_words<true>(a.ref, s, out);
+    const uint32_t declared = a.kind_len & 0xFFFFFFu;
+    if (use_pre) put_unix_words<true>(*pre, s, out, dc, declared);
+    else put_unix_words<true>(a.ref, s, out, dc, declared);
 }
 
 // CallBody::serialise_into (call_body.rs:98-108) up to the raw payload.
 template <class Sink>
 __device__ __forceinline__ void put_call_words(const onc_msg& d, const EncSrc& s, Sink& out,
-                                               const UnixRegs* cred_pre = nullptr, bool use_pre = false) {
+                                               const UnixRegs* cred_pre = nullptr, bool use_pre = false,
+                                               DeclCheck* dc = nullptr) {
     out(bswap(2u));                           // RPC_VERSION call_body.rs:10
     out(bswap(d.u.call.program));
     out(bswap(d.u.call.program_version));
     out(bswap(d.u.call.procedure));
-    put_auth_words(d.cred, s, out, cred_pre, use_pre);
-    put_auth_words(d.verf, s, out);
+    put_auth_words(d.cred, s, out, cred_pre, use_pre, dc);
+    if (dc && dc->st != ONC_OK) return;
+    put_auth_words(d.verf, s, out, nullptr, false, dc);
 }
 
 // AcceptedStatus::serialise_into (accepted_reply.rs:195-211) up to a
@@ -368,10 +431,12 @@ __device__ __forceinline__ void put_rejected_words(const onc_msg& d, Sink& out) 
 // ReplyBody::serialise_into (reply_body.rs:45-56; AcceptedReply
 // accepted_reply.rs:58-61) up to a Success payload.
 template <class Sink>
-__device__ __forceinline__ void put_reply_words(const onc_msg& d, const EncSrc& s, Sink& out) {
+__device__ __forceinline__ void put_reply_words(const onc_msg& d, const EncSrc& s, Sink& out,
+                                                DeclCheck* dc = nullptr) {
     out(bswap(uint32_t(d.reply_stat)));
     if (d.reply_stat == ONC_REPLY_ACCEPTED) {
-        put_auth_words(d.verf, s, out);
+        put_auth_words(d.verf, s, out, nullptr, false, dc);
+        if (dc && dc->st != ONC_OK) return;
         put_accepted_status_words(d, out);
         return;
     }
@@ -381,14 +446,16 @@ __device__ __forceinline__ void put_reply_words(const onc_msg& d, const EncSrc& 
 // RpcMessage::serialise_into (rpc_message.rs:136-164; MessageType :55-68)
 // up to the raw payload.
 // (cred_pre, when use_pre: the Call's AUTH_UNIX credential block, already loaded)
+// (dc: run the deferred checks of declared AUTH_UNIX auths, plan_record<true>)
 template <class Sink>
 __device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, Sink& out,
-                                                 const UnixRegs* cred_pre = nullptr, bool use_pre = false) {
+                                                 const UnixRegs* cred_pre = nullptr, bool use_pre = false,
+                                                 DeclCheck* dc = nullptr) {
     out(bswap((len - 4u) | 0x80000000u));        // record mark, rpc_message.rs:156
     out(bswap(d.xid));
     out(bswap(uint32_t(d.msg_type)));
-    if (d.msg_type == ONC_MSG_CALL) put_call_words(d, s, out, cred_pre, use_pre);
-    else put_reply_words(d, s, out);
+    if (d.msg_type == ONC_MSG_CALL) put_call_words(d, s, out, cred_pre, use_pre, dc);
+    else put_reply_words(d, s, out, dc);
 }
 
 __device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, uint32_t* dst) {

@@ -53,11 +53,22 @@ __global__ __launch_bounds__(kLenThreads) void enc_len_kernel(EncArgs a) {
         const uint64_t r = rw + 64 * k + lane;
         uint64_t len = 0, pay = 0;
         if (r < a.n) {
-            const RecPlan p = kRoot ? plan_root(d[k], a.unix, a.bounds, a.root) : plan_record(d[k], a.unix, a.bounds);
+            RecPlan p;
+            if (kRoot) {
+                p = plan_root(d[k], a.unix, a.bounds, a.root);
+            } else {
+                // the plan of an emit takes declared AUTH_UNIX lengths as
+                // given (no parameter-block load: the emit checks the block);
+                // a record failing that form is planned in full for its
+                // reference-order status (rare: only failing records)
+                if (a.decl) p = plan_record<true>(d[k], a.unix, a.bounds);
+                if (!a.decl || p.status != ONC_OK) p = plan_record<false>(d[k], a.unix, a.bounds);
+            }
             len = p.len;
             pay = len - 4ull * meta_hw(p.meta);           // 0 for a failing record (len = meta = 0)
             a.status[r] = p.status;
             if (a.rec_len) a.rec_len[r] = uint32_t(len);
+            if (a.len_out) a.len_out[r] = uint32_t(len);
         }
         const uint64_t incl = wave_incl_scan_u64(len);
         const uint64_t tile = (rw + 64 * k) / kEmitRecs;
@@ -270,6 +281,18 @@ struct ImgSink {
             __hip_atomic_fetch_or(img32 + img_dword(d), prev >> sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
 };
+
+// Clear bytes [b, b + n) of the image (the header words of a record that
+// failed a deferred check, already ORed in): the neighbours' bytes in the
+// two edge dwords stay.
+__device__ __forceinline__ void img_clear(uint32_t* img32, uint32_t b, uint32_t n) {
+    const uint32_t e = b + n;
+    for (uint32_t dw = b >> 2; 4 * dw < e; ++dw) {
+        const uint32_t lo = max(b, 4 * dw) - 4 * dw, hi = min(e, 4 * dw + 4) - 4 * dw;   // bytes [lo, hi) of the dword
+        const uint32_t m = (hi == 4 ? ~0u : (1u << (8 * hi)) - 1u) & ~((1u << (8 * lo)) - 1u);
+        __hip_atomic_fetch_and(img32 + img_dword(dw), ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+}
 
 // One chunk of the word path: dword i is payload (sel bit i) taken from the
 // rotated load, else the image dword.
@@ -579,8 +602,9 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                                d.stat == ONC_ACCEPT_SUCCESS);
             hw = len ? uint32_t((len - (body ? uint64_t(d.payload_len) : 0ull)) >> 2) : 0;
         } else {
-            // the same function as enc_len: lengths agree
-            const RecPlan p = kRoot ? plan_root(d, a.unix, a.bounds, a.root) : plan_record(d, a.unix, a.bounds);
+            // the same function as enc_len: lengths agree (declared AUTH_UNIX
+            // lengths: no parameter-block load here)
+            const RecPlan p = kRoot ? plan_root(d, a.unix, a.bounds, a.root) : plan_record<true>(d, a.unix, a.bounds);
             len = p.len;
             hw = len ? meta_hw(p.meta) : 0;
         }
@@ -592,7 +616,8 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     const uint64_t en = start + len;
     const uint64_t pst = start + 4ull * hw;
     if (lane < nrec) {
-        a.rec_off[r0 + lane] = start - a.origin;
+        // (a chunk's first offset is the base it read: the previous chunk wrote it)
+        if (r0 + lane != 0 || !a.base_dev) a.rec_off[r0 + lane] = start - a.origin;
         if (r0 + lane + 1 == a.n) a.rec_off[a.n] = en - a.origin;   // the grand total
         if (len != 0 && en > a.out_cap) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
     }
@@ -665,8 +690,21 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                 const onc_msg d = as_msg(mr2);
                 const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
                 ImgSink w{img32, uint32_t(ibb >> 2), 32u - 8u * uint32_t(ibb & 3), 0u};
-                if (kRoot) put_root_words(d, uint32_t(len), src, a.root, w);
-                else put_header_words(d, uint32_t(len), src, w, &cq, cred_unix);
+                // declared AUTH_UNIX lengths: the parameter-block checks the
+                // plan deferred run on the block words the serialiser loads;
+                // a failing record keeps its extent with its header words
+                // cleared (include/onc_rpc.h onc_auth)
+                DeclCheck dc{a.bounds.auth_len, ONC_OK};
+                if (kRoot) {
+                    put_root_words(d, uint32_t(len), src, a.root, w);
+                } else {
+                    put_header_words(d, uint32_t(len), src, w, &cq, cred_unix, &dc);
+                    if (dc.st != ONC_OK) {
+                        a.status[r0 + lane] = dc.st;
+                        img_clear(img32, uint32_t(ibb), 4 * hw);
+                        w.prev = 0u;
+                    }
+                }
                 if (small) {
                     // all of it lies in non-pure chunks (np = 0): right after
                     // the header (bytes past its end read as zero)
@@ -793,7 +831,7 @@ __device__ __forceinline__ void ws_begin_tile(const EncArgs& a, WsTile& S, WsLan
     uint32_t hw = 0;
     bool word_aligned = true;
     if (lane < S.nrec) {
-        const RecPlan p = plan_record(dm, a.unix, a.bounds);
+        const RecPlan p = plan_record<true>(dm, a.unix, a.bounds);
         len = p.len;
         hw = len ? meta_hw(p.meta) : 0;
         poff = dm.payload_off;
@@ -804,7 +842,8 @@ __device__ __forceinline__ void ws_begin_tile(const EncArgs& a, WsTile& S, WsLan
     const uint64_t en = start + len;
     const uint64_t pst = start + 4ull * hw;
     if (lane < S.nrec) {
-        a.rec_off[S.r0 + lane] = start - a.origin;
+        // (a chunk's first offset is the base it read: the previous chunk wrote it)
+        if (S.r0 + lane != 0 || !a.base_dev) a.rec_off[S.r0 + lane] = start - a.origin;
         if (S.r0 + lane + 1 == a.n) a.rec_off[a.n] = en - a.origin;
         if (len != 0 && en > a.out_cap) a.status[S.r0 + lane] = ONC_ENC_WRITE_ZERO;
     }
@@ -867,7 +906,13 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
             const onc_msg d = as_msg(mr2);
             const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
             ImgSink w{img32, uint32_t(ibb >> 2), 32u - 8u * uint32_t(ibb & 3), 0u};
-            put_header_words(d, uint32_t(Slen), src, w);
+            DeclCheck dc{a.bounds.auth_len, ONC_OK};
+            put_header_words(d, uint32_t(Slen), src, w, nullptr, false, &dc);
+            if (dc.st != ONC_OK) {                     // (see enc_emit_tile)
+                a.status[S.r0 + lane] = dc.st;
+                img_clear(img32, uint32_t(ibb), uint32_t(Spst - Sstart));
+                w.prev = 0u;
+            }
             if (small) {
                 const uintptr_t pb = sb + Spst;
                 for (uint32_t k = 0; 4 * k < Splen; ++k) w(load4_masked(pb + 4 * k, pb + Splen));
@@ -1008,7 +1053,8 @@ static_assert(kWsGrid / kTilesPerBlk <= 64, "a producer adds at most 64 workgrou
 // the grid's waves), placed by a running sum of the enc_len workgroup
 // totals, as the producer does.
 constexpr uint64_t kWsMinPayload = 128;     // bytes per record (the host rule's threshold)
-constexpr uint64_t kWsSample = 64;          // enc_len workgroups sampled (64k records)
+constexpr uint64_t kWsSample = 1024;        // enc_len workgroups summed (all of them up to 1M records — one
+                                            // chunk of a chunked encode — else every ceil(nb / 1024)-th)
 union WsShared {
     struct {
         WsSlot slot[2];
@@ -1017,13 +1063,29 @@ union WsShared {
     ImgTile wpt[4];
 };
 
+// The whole launch's payload, not its head (round 3 sampled the first 64
+// workgroups, so a batch whose head and tail differ got the wrong kernel):
+// 16 loads per lane, issued together — the same one round trip.
 __device__ __forceinline__ bool ws_header_heavy(const EncArgs& a) {
-    if (!a.block_pay || (a.variant & 0x10000)) return false;     // 0x10000: the pipeline on every shape (tests)
+    if (!a.block_pay || (a.variant & ONC_VARIANT_WS_PIPELINE)) return false;   // the pipeline on every shape (tests)
     const int lane = threadIdx.x & 63;
     const uint64_t nb = num_len_blocks(a.n);
-    const uint64_t pay = uint64_t(lane) < min(nb, kWsSample) ? a.block_pay[lane] : 0;
-    const uint64_t recs = min(a.n, kWsSample * kLenRecs);
-    return lane_u64(wave_incl_scan_u64(pay), 63) < kWsMinPayload * recs;
+    const uint64_t stride = (nb + kWsSample - 1) / kWsSample;
+    constexpr int kPer = int(kWsSample / 64);
+    uint64_t v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint64_t b = (uint64_t(lane) + 64ull * k) * stride;
+        v[k] = a.block_pay[b < nb ? b : nb - 1];
+    }
+    uint64_t pay = 0, recs = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint64_t b = (uint64_t(lane) + 64ull * k) * stride;
+        pay += b < nb ? v[k] : 0;
+        recs += b < nb ? min(uint64_t(kLenRecs), a.n - b * kLenRecs) : 0;
+    }
+    return lane_u64(wave_incl_scan_u64(pay), 63) < kWsMinPayload * lane_u64(wave_incl_scan_u64(recs), 63);
 }
 
 template <int kU, int kNT>
@@ -1094,9 +1156,9 @@ __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
         } else if (state == 1u) {
             const SpanHdr h = s_slot[cur].h;
             if (h.byte_mode) stream_span_part<1, kNT, true>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
-            else if (h.interior == 2 && !(a.variant & 0x8000))
+            else if (h.interior == 2 && !(a.variant & ONC_VARIANT_WS_NO_FULL))
                 stream_span_part<kU, kNT, false, 2>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
-            else if (h.interior && !(a.variant & 0x4000))
+            else if (h.interior && !(a.variant & ONC_VARIANT_WS_NO_INTERIOR))
                 stream_span_part<kU, kNT, false, 1>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
             else stream_span_part<kU, kNT, false>(a, s_slot[cur].T, h, wv - 1, 3, dummy);
         }
@@ -1127,10 +1189,12 @@ __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
 // kNT: bit 0 = nontemporal payload loads, bit 1 = nontemporal stores (header
 // chunks stored temporally so that the decoder finds them cached made the
 // decode slower, 60 -> 69 us on c1: the dirty lines are written back at the
-// kernel boundary). Registers are left free (102 VGPRs, 4 waves per SIMD):
-// squeezed to 5 waves per SIMD every shape measured slower (spills).
+// kernel boundary). The message instances are held to 4 waves per SIMD (128
+// VGPRs, no spills; the deferred AUTH_UNIX checks took them to 134, 3 waves);
+// squeezed to 5 waves per SIMD every shape measured slower (spills). The
+// body-root instances keep what they need (138 VGPRs).
 template <int kU, int kNT = 0, bool kFused = false, bool kRoot = false, bool kLen = false>
-__global__ __launch_bounds__(64 * kFastWaves) void enc_emit_kernel_t(EncArgs a) {
+__global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(kRoot ? 1 : 4))) void enc_emit_kernel_t(EncArgs a) {
     __shared__ ImgTile s_tiles[kFastWaves];
     const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
     if (tile < num_emit_tiles(a.n))

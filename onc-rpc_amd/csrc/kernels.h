@@ -47,15 +47,18 @@ struct EncArgs {
     uint64_t* rec_off;      // n + 1
     int32_t* status;        // n
     uint32_t* rec_len;      // n, optional
+    uint32_t* len_out;      // enc_len: optional codec-owned copy of the lengths (what the emit reads back)
     uint64_t* tile_sum;     // tiles
     uint64_t* block_sum;    // enc_len workgroups (kLenRecs records): byte totals
     uint64_t* block_base;   // exclusive scan of block_sum (unused when fused_base)
     uint64_t* block_pay;    // optional: enc_len workgroups' streamed payload bytes (the wave-specialised
                             // enc_emit's header-heavy test); NULL = not computed
     uint32_t fused_base;    // enc_emit sums block_sum itself (<= kFusedBlocks workgroups; no scan launch)
-    uint32_t variant;       // ONC_RPC_VARIANT bits (A/B experiments)
+    uint32_t variant;       // ONC_VARIANT_* bits (onc_codec_options; A/B experiments, tests)
     uint32_t ws;            // enc_emit: the wave-specialised kernel (codec.hip enc_args decides)
     uint32_t root;          // ONC_ROOT_* (onc_encode_body); ONC_ROOT_RPC_MESSAGE for onc_encode
+    uint32_t decl;          // enc_len of an emit's plan: declared AUTH_UNIX lengths taken as given (the
+                            // emit runs the deferred parameter-block checks); 0: every check (onc_encode_lengths)
     const uint64_t* base_dev;   // optional: output bytes before this launch's first record (chunked encode)
     const uint32_t* len_in;     // optional (wave-per-tile enc_emit): the plan's record lengths, read instead
                                 // of re-planning (no dependent AUTH_UNIX parameter load in the prologue)
@@ -122,7 +125,7 @@ struct DecArgs {
     const uint8_t* wire;
     const uint64_t* rec_off;
     onc_decoded out;
-    uint32_t variant;       // ONC_RPC_VARIANT bits (A/B experiments)
+    uint32_t variant;       // ONC_VARIANT_* bits (onc_codec_options)
     // onc_decode_lengths: offsets from the lengths inside the decode
     const uint32_t* rec_len;
     const uint64_t* tile_sum;   // per decode workgroup (kDecTile records): byte total
@@ -167,6 +170,7 @@ hipError_t launch_len_tiles(const uint32_t* len, uint64_t n, uint64_t* tile_sum,
 hipError_t launch_len_apply(const uint32_t* len, uint64_t n, const uint64_t* tile_base, uint64_t* rec_off,
                             hipStream_t s);
 bool scan_lengths_fused_ok(uint64_t n);
+hipError_t launch_store_u64(uint64_t* p, uint64_t v, hipStream_t s);
 hipError_t launch_lenblk(const uint32_t* len, uint64_t n, uint64_t* blk_sum, hipStream_t s);
 hipError_t launch_lenoff(const uint32_t* len, uint64_t n, const uint64_t* blk_sum, uint64_t base, uint64_t* rec_off,
                          hipStream_t s);

@@ -180,6 +180,15 @@ hipError_t launch_len_apply(const uint32_t* len, uint64_t n, const uint64_t* til
     return hipGetLastError();
 }
 
+// rec_off[0] = base of an empty scan (a kernel rather than a copy from the
+// host stack: no synchronisation, capturable)
+__global__ void store_u64_kernel(uint64_t* p, uint64_t v) { *p = v; }
+
+hipError_t launch_store_u64(uint64_t* p, uint64_t v, hipStream_t s) {
+    ONC_LAUNCH(store_u64_kernel, dim3(1), dim3(1), 0, s, p, v);
+    return hipGetLastError();
+}
+
 bool scan_lengths_fused_ok(uint64_t n) { return (n + kLenBlk - 1) / kLenBlk <= kLenBlkMax; }
 
 hipError_t launch_lenblk(const uint32_t* len, uint64_t n, uint64_t* blk_sum, hipStream_t s) {

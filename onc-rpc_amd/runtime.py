@@ -23,7 +23,7 @@ K_NAMES = ["enc_len_kernel", "scan_tiles_kernel", "enc_emit_kernel", "decode_ker
            "frame_counts_kernel", "frame_guess_kernel"]
 (K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY, K_IOV_LEN,
  K_IOV_EMIT, K_FRAME, K_FRAME_WRITE, K_FRAME_WALK, K_FRAME_COUNTS, K_FRAME_GUESS) = range(13)
-ABI_VERSION = 5
+ABI_VERSION = 6
 K_COUNT = len(K_NAMES)
 
 # every symbol include/onc_rpc.h declares
@@ -34,13 +34,28 @@ EXPORTED = [
     "onc_kernel_name", "onc_encode_lengths", "onc_encode", "onc_decode", "onc_scan_lengths",
     "onc_expected_message_len", "onc_encode_iov", "onc_frame_stream", "onc_encode_plan", "onc_encode_emit",
     "onc_decode_lengths", "onc_decode_body", "onc_encode_body", "onc_encode_body_lengths",
+    "onc_codec_create_ex", "onc_codec_set_decode_policy",
 ]
+
+# onc_codec_options (include/onc_rpc.h)
+DECODE_POLICY_AUTO, DECODE_POLICY_STANDARD, DECODE_POLICY_LINE = 0, 1, 2
+OPT_FORCE_SCAN = 0x1
+VARIANT_EMIT_WS, VARIANT_EMIT_TILE = 0x200, 0x400
+VARIANT_WS_NO_INTERIOR, VARIANT_WS_NO_FULL, VARIANT_WS_PIPELINE = 0x4000, 0x8000, 0x10000
+VARIANT_EMIT_REPLAN, VARIANT_WHOLE_PLAN = 0x20000, 0x40000
+# options every Codec() gets unless it is given its own (bench.py --variant)
+DEFAULT_OPTIONS: dict = {}
 
 
 class OncBatch(C.Structure):
     _fields_ = [("n", C.c_uint64), ("msgs", C.c_void_p), ("unix_params", C.c_void_p),
                 ("auth_arena", C.c_void_p), ("payload_arena", C.c_void_p),
                 ("unix_count", C.c_uint64), ("auth_len", C.c_uint64), ("payload_len", C.c_uint64)]
+
+
+class OncCodecOptions(C.Structure):
+    _fields_ = [("size", C.c_uint32), ("flags", C.c_uint32), ("decode_policy", C.c_int32), ("variant", C.c_uint32),
+                ("enc_chunk", C.c_uint64), ("frame_chunk", C.c_uint64)]
 
 
 class OncDecoded(C.Structure):
@@ -63,6 +78,8 @@ def load_library(path=LIB_PATH):
     vp, u64, i32 = C.c_void_p, C.c_uint64, C.c_int
     lib.onc_abi_version.restype = i32
     lib.onc_codec_create.argtypes = [C.POINTER(vp), i32, vp]
+    lib.onc_codec_create_ex.argtypes = [C.POINTER(vp), i32, vp, C.POINTER(OncCodecOptions)]
+    lib.onc_codec_set_decode_policy.argtypes = [vp, i32]
     lib.onc_codec_destroy.argtypes = [vp]
     lib.onc_codec_set_stream.argtypes = [vp, vp]
     lib.onc_codec_sync.argtypes = [vp]
@@ -154,11 +171,18 @@ class DeviceBatch:
                         self.unix_count, self.auth_len, self.payload_len)
 
 
+def codec_options(variant=0, force_scan=False, enc_chunk=0, frame_chunk=0, decode_policy=DECODE_POLICY_AUTO):
+    """onc_codec_options (include/onc_rpc.h) from keyword arguments."""
+    return OncCodecOptions(C.sizeof(OncCodecOptions), OPT_FORCE_SCAN if force_scan else 0, decode_policy, variant,
+                           enc_chunk, frame_chunk)
+
+
 class Codec:
     """One onc_codec handle bound to a device and (by default) torch's
-    current stream on that device."""
+    current stream on that device. `options`: keyword arguments of
+    codec_options (default: DEFAULT_OPTIONS)."""
 
-    def __init__(self, device=0, stream=None):
+    def __init__(self, device=0, stream=None, **options):
         torch = _torch()
         self.lib = load_library()
         self.device = device
@@ -166,10 +190,19 @@ class Codec:
             stream = torch.cuda.current_stream(device).cuda_stream
         self.stream = stream
         h = C.c_void_p()
-        rc = self.lib.onc_codec_create(C.byref(h), device, C.c_void_p(stream))
+        opt = codec_options(**(options or DEFAULT_OPTIONS))
+        rc = self.lib.onc_codec_create_ex(C.byref(h), device, C.c_void_p(stream), C.byref(opt))
         if rc != 0:
-            raise CodecError(f"onc_codec_create rc={rc}")
+            raise CodecError(f"onc_codec_create_ex rc={rc}")
         self.h = h
+
+    def set_stream(self, stream):
+        """Bind the handle to another HIP stream (an int hipStream_t or a torch stream)."""
+        self.stream = getattr(stream, "cuda_stream", stream)
+        self._check(self.lib.onc_codec_set_stream(self.h, C.c_void_p(self.stream)), "onc_codec_set_stream")
+
+    def set_decode_policy(self, policy):
+        self._check(self.lib.onc_codec_set_decode_policy(self.h, policy), "onc_codec_set_decode_policy")
 
     def close(self):
         if self.h:

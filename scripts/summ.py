@@ -11,4 +11,4 @@ for f in sys.argv[1:]:
     k = d["kernels_breakdown_pass"]
     print(f, round(d["value"], 1), round(d["ms_per_step"] * 1e3, 1), "us/step",
           {n: round(v["avg_us"] * v.get("launches_per_step", 1), 1) for n, v in k.items()}, "us/step per kernel;",
-          "frac", round(d["roofline"]["frac"], 3), d["roofline"]["kernel"])
+          "frac", round(d["roofline"]["frac"], 3), d["roofline"]["kernel"], round(d["roofline"]["avg_launch_us"], 1), "us")

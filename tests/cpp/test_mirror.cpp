@@ -6,6 +6,7 @@
 // see tests/golden/make_golden.py). Run by tests/test_cpp_mirror.py (-m gpu).
 //
 // Usage: test_mirror <path to vectors.json>
+#include <chrono>
 #include <cstdio>
 #include <fstream>
 #include <functional>
@@ -173,6 +174,46 @@ static void test_bench_message_round_trip(Codec& c) {
     CHECK(back.call_body()->auth_credentials() == msg.call_body()->auth_credentials());
     CHECK(back.call_body()->payload() == Bytes(payload));
     CHECK(back == msg);
+}
+
+// What the single-message calls cost (onc_rpc.hpp): RpcMessage::serialise /
+// try_from on a Codec are whole GPU round trips (host arenas -> device,
+// kernels, device -> host, a stream sync each), meant for tests and tiny
+// batches; BatchEncoder / BatchDecoder amortise that over a batch. The
+// configs[0] message (benches/bench.rs:86-101): 200 single-message round
+// trips against one 200-message batch round trip, printed as TIMING lines.
+static void test_single_message_cost(Codec& c) {
+    std::vector<uint8_t> payload(64);
+    for (size_t i = 0; i < payload.size(); ++i) payload[i] = uint8_t(i * 5 + 1);
+    const RpcMessage msg(7, MessageType::call(CallBody(100000, 42, 13,
+                                                       AuthFlavor::unix(AuthUnixParams(0, Bytes(), 501, 20, gids16())),
+                                                       AuthFlavor::none(), Bytes(payload))));
+    constexpr int kN = 200;
+    (void)RpcMessage::try_from(c, Bytes(msg.serialise(c)));     // warm-up
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < kN; ++i) {
+        const std::vector<uint8_t> w = msg.serialise(c);
+        CHECK(RpcMessage::try_from(c, Bytes(w)) == msg);
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    BatchEncoder enc;
+    for (int i = 0; i < kN; ++i) enc.push(msg);
+    std::vector<uint8_t> wire;
+    std::vector<uint64_t> off;
+    (void)enc.serialise_into(c, wire, &off);                     // warm-up
+    const auto t2 = std::chrono::steady_clock::now();
+    wire.clear();
+    const std::vector<int32_t> st = enc.serialise_into(c, wire, &off);
+    std::vector<uint32_t> rec_len(kN);
+    for (int i = 0; i < kN; ++i) rec_len[i] = uint32_t(off[i + 1] - off[i]);
+    BatchDecoder dec;
+    const std::vector<Decoded> out = dec.try_from(c, wire.data(), wire.size(), rec_len);
+    const auto t3 = std::chrono::steady_clock::now();
+    for (int i = 0; i < kN; ++i) CHECK(st[i] == ONC_OK && out[i].ok() && *out[i].message == msg);
+    const double single = std::chrono::duration<double, std::micro>(t1 - t0).count() / kN;
+    const double batch = std::chrono::duration<double, std::micro>(t3 - t2).count();
+    std::printf("TIMING single_message_round_trip_us=%.1f batch_%d_round_trip_us=%.1f per_message_in_batch_us=%.2f\n",
+                single, kN, batch, batch / kN);
 }
 
 // Panic parity: flavor.rs:110 (assoc > 200), unix_params.rs:149 (name > 255),
@@ -492,6 +533,7 @@ int main(int argc, char** argv) {
         {"test_auth_opaque_flavors", test_auth_opaque_flavors},
         {"test_auth_unix_params", test_auth_unix_params},
         {"test_body_types", test_body_types},
+        {"test_single_message_cost", test_single_message_cost},
     };
     for (const auto& t : tests) {
         try {

@@ -4,7 +4,7 @@ rpc_message.rs:235-314, over the rpc_message.rs:238-242 slicing contract) —
 bit-exact against the CPU oracle and identical to onc_scan_lengths +
 onc_decode, in both modes, with the block totals summed in the kernel
 (<= 2M records) and scanned by a separate launch (forced here with
-ONC_RPC_FORCE_SCAN), at a non-zero base offset, on corrupted records and at
+ONC_OPT_FORCE_SCAN), at a non-zero base offset, on corrupted records and at
 workgroup / block boundaries."""
 import numpy as np
 import pytest
@@ -30,12 +30,7 @@ def codec(request, R):
     import os
     import torch
     assert torch.cuda.is_available(), "GPU tests need an MI355X"
-    if request.param == "scan":
-        os.environ["ONC_RPC_FORCE_SCAN"] = "1"
-    try:
-        c = R.Codec(0)
-    finally:
-        os.environ.pop("ONC_RPC_FORCE_SCAN", None)
+    c = R.Codec(0, force_scan=request.param == "scan")
     yield c
     c.close()
 

@@ -1,4 +1,4 @@
-"""Both enc_emit kernels, forced (ONC_RPC_VARIANT 0x200: the wave-specialised
+"""Both enc_emit kernels, forced (onc_codec_options.variant 0x200: the wave-specialised
 producer/consumer kernel; 0x400: the wave-per-tile kernel), bit-exact against
 the CPU oracle (RpcMessage::serialise_into, rpc_message.rs:136-164) on the
 batch shapes that stress placement and staging: many tiles per persistent
@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 # wave-per-tile workers (encode.hip ws_header_heavy); ws_pipeline: the same
 # kernel with that fallback off (0x10000), its producer/consumer pipeline
 # on every shape; tile: the wave-per-tile kernel
-PATHS = {"ws": "0x200", "ws_pipeline": "0x10200", "tile": "0x400"}
+PATHS = {"ws": 0x200, "ws_pipeline": 0x10200, "tile": 0x400}
 
 
 @pytest.fixture(scope="module")
@@ -34,15 +34,7 @@ def codec(request, R):
     import os
     import torch
     assert torch.cuda.is_available(), "GPU tests need an MI355X"
-    old = os.environ.get("ONC_RPC_VARIANT")
-    os.environ["ONC_RPC_VARIANT"] = PATHS[request.param]
-    try:
-        c = R.Codec(0)
-    finally:
-        if old is None:
-            del os.environ["ONC_RPC_VARIANT"]
-        else:
-            os.environ["ONC_RPC_VARIANT"] = old
+    c = R.Codec(0, variant=PATHS[request.param])
     yield c
     c.close()
 

@@ -408,15 +408,13 @@ def test_full_size_loopback_idempotent(codec, R, oracle, cfg):
         assert_decoded_equal(g, o, f"{cfg} window")
 
 
-def test_block_base_scan_path(R, oracle, monkeypatch):
+def test_block_base_scan_path(R, oracle):
     """Encode places tiles either from enc_emit's own sum of the enc_len
     workgroup totals (<= 1024 workgroups) or from the scan kernel: the
     forced-scan codec and a batch above the fused limit (1.1M records) are
     bit-exact vs the oracle as well."""
     hb = S.mixed(6000, seed=21, pmin=0, pmax=700, exotic=0.2)
-    monkeypatch.setenv("ONC_RPC_FORCE_SCAN", "1")
-    c_scan = R.Codec(0)
-    monkeypatch.delenv("ONC_RPC_FORCE_SCAN")
+    c_scan = R.Codec(0, force_scan=True)
     try:
         gpu_vs_oracle_encode(R, c_scan, oracle, hb)
     finally:
@@ -573,18 +571,17 @@ def _frame_both(R, codec, oracle, buf, max_records=None):
 
 
 @pytest.fixture(params=[None, 64, 1024, "force_scan"])
-def frame_codec(request, R, monkeypatch):
+def frame_codec(request, R):
     """Codec with the default framing chunk (64 KiB) and with small chunks
-    (ONC_RPC_FRAME_CHUNK), so that test streams span many chunks: guesses,
+    (onc_codec_options.frame_chunk), so that test streams span many chunks: guesses,
     verification and the walk across chunk boundaries; "force_scan" takes the
-    three-launch count scan (ONC_RPC_FORCE_SCAN=1) instead of the fused one."""
+    three-launch count scan (onc_codec_options ONC_OPT_FORCE_SCAN) instead of the fused one."""
     if request.param == "force_scan":
-        monkeypatch.setenv("ONC_RPC_FORCE_SCAN", "1")
+        c = R.Codec(0, force_scan=True)
     elif request.param is not None:
-        monkeypatch.setenv("ONC_RPC_FRAME_CHUNK", str(request.param))
-    c = R.Codec(0)
-    monkeypatch.delenv("ONC_RPC_FRAME_CHUNK", raising=False)
-    monkeypatch.delenv("ONC_RPC_FORCE_SCAN", raising=False)
+        c = R.Codec(0, frame_chunk=request.param)
+    else:
+        c = R.Codec(0)
     yield c
     c.close()
 

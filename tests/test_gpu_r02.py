@@ -315,19 +315,11 @@ def test_two_ranks_hip_codec_concatenate(codec, R, oracle, tmp_path):
 @pytest.mark.parametrize("force", [False, True])
 def test_scan_lengths_sizes_and_alignment(R, force):
     """onc_scan_lengths: the two-launch path (lenblk -> lenoff, up to 8M
-    records) and the three-launch path (ONC_RPC_FORCE_SCAN=1, or beyond 8M)
+    records) and the three-launch path (ONC_OPT_FORCE_SCAN, or beyond 8M)
     at block boundaries, with misaligned length / offset pointers (slices):
     rec_off = base + exclusive prefix sum, rec_off[n] = base + total."""
     import torch
-    old = os.environ.get("ONC_RPC_FORCE_SCAN")
-    os.environ["ONC_RPC_FORCE_SCAN"] = "1" if force else "0"
-    try:
-        c = R.Codec(0)
-    finally:
-        if old is None:
-            del os.environ["ONC_RPC_FORCE_SCAN"]
-        else:
-            os.environ["ONC_RPC_FORCE_SCAN"] = old
+    c = R.Codec(0, force_scan=force)
     rng = np.random.default_rng(11)
     sizes = [1, 15, 16, 17, 4095, 4096, 4097, 8191, 65536 + 3, 2048 * 4096, 2048 * 4096 + 1]
     for n in sizes:

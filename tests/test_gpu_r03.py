@@ -107,7 +107,7 @@ def test_emit_needs_the_plans_status_array(codec, R, oracle):
 
 @pytest.mark.parametrize("variant", [0x200, 0x400, 0x200 | 0x4000, 0x200 | 0x8000])
 @pytest.mark.parametrize("layout", ["first_last", "reversed"])
-def test_payloads_at_arena_edges(R, oracle, monkeypatch, variant, layout):
+def test_payloads_at_arena_edges(R, oracle, variant, layout):
     """Payloads starting at byte 0 and ending at the last byte of a payload
     arena declared exactly as large as its payloads (and placed at the very
     end of its tensor): the interior-span source check (encode.hip
@@ -115,8 +115,7 @@ def test_payloads_at_arena_edges(R, oracle, monkeypatch, variant, layout):
     bit-exact on the wave-specialised kernel (0x200, with and without the
     interior / full-interior paths) and the wave-per-tile one (0x400)."""
     import torch
-    monkeypatch.setenv("ONC_RPC_VARIANT", str(variant))
-    codec = R.Codec(0)
+    codec = R.Codec(0, variant=variant)
     try:
         rng = np.random.default_rng(variant + (7 if layout == "reversed" else 0))
         n = 3000
@@ -262,19 +261,18 @@ def test_decode_at_every_record_alignment(codec, R, oracle, gen):
         assert int((g[2] == 0).sum()) == hb.n
 
 
-@pytest.mark.parametrize("variant", [0, 0x80000, 0x100000])
-def test_decode_line_policy(R, oracle, monkeypatch, variant):
+@pytest.mark.parametrize("policy", [0, 2, 1])
+def test_decode_line_policy(R, oracle, policy):
     """The decode's two first-round policies (decode.hip kLine1Min): the line
-    policy (0x80000: round 1 takes the rest of the record's first 128-byte
-    line), the standard one (0x100000), and the automatic choice from the
-    codec's hint word (0: a unix16 batch flips it to the line policy for the
-    next launch, a mixed one back). Every launch bit-exact vs the oracle in
+    policy (ONC_DECODE_POLICY_LINE: round 1 takes the rest of the record's
+    first 128-byte line), the standard one (_STANDARD), and the automatic
+    choice from the codec's hint word (_AUTO: a unix16 batch flips it to the
+    line policy for the next launch, a mixed one back). Every launch bit-exact vs the oracle in
     both modes: header-heavy and mixed batches at every record alignment,
     records cut inside their first line (truncated headers), and the
     lengths-driven decode."""
     import torch
-    monkeypatch.setenv("ONC_RPC_VARIANT", str(variant))
-    codec = R.Codec(0)
+    codec = R.Codec(0, decode_policy=policy)
     try:
         unix16 = S.call_unix16(1200, 40, seed=41)
         mixed = S.mixed(1200, seed=42, pmin=0, pmax=300, exotic=0.2)
@@ -286,10 +284,10 @@ def test_decode_line_policy(R, oracle, monkeypatch, variant):
                 o2 = off.astype(np.uint64) + np.uint64(shift)
                 for mode in (L.DECODE_SLICE, L.DECODE_BYTES):
                     _same_decode(R.decode_host_wire(codec, w, o2, mode), oracle.decode_batch(w, o2, mode),
-                                 f"variant {variant:#x} shift {shift} mode {mode}")
+                                 f"policy {policy} shift {shift} mode {mode}")
             # every record cut to a prefix (1..200 bytes): headers that end
             # inside the first line, inside round 1, or past the window
-            rng = np.random.default_rng(variant + 1)
+            rng = np.random.default_rng(policy + 1)
             recs = []
             for i in range(hb.n):
                 r = bytes(base[int(off[i]):int(off[i + 1])])
@@ -297,7 +295,7 @@ def test_decode_line_policy(R, oracle, monkeypatch, variant):
             w2, o3 = L.records_from_wire(recs)
             for mode in (L.DECODE_SLICE, L.DECODE_BYTES):
                 _same_decode(R.decode_host_wire(codec, w2, o3, mode), oracle.decode_batch(w2, o3, mode),
-                             f"variant {variant:#x} truncated mode {mode}")
+                             f"policy {policy} truncated mode {mode}")
             # lengths-driven decode of the same wire
             n = hb.n
             lens = np.diff(off.astype(np.int64)).astype(np.uint32)
@@ -309,14 +307,14 @@ def test_decode_line_policy(R, oracle, monkeypatch, variant):
                                  rec_off=ro)
             codec.sync()
             _same_decode(dec.to_host(), oracle.decode_batch(base, off.astype(np.uint64), L.DECODE_SLICE),
-                         f"variant {variant:#x} decode_lengths")
+                         f"policy {policy} decode_lengths")
     finally:
         codec.close()
 
 
 @pytest.mark.parametrize("variant", [0x400, 0x400 | 0x20000])
 @pytest.mark.parametrize("given_len", [False, True])
-def test_emit_from_plan_lengths(R, oracle, monkeypatch, variant, given_len):
+def test_emit_from_plan_lengths(R, oracle, variant, given_len):
     """The wave-per-tile enc_emit reads the plan's record lengths (the
     caller's rec_len, or the codec's own array) instead of planning again
     when the batch has an AUTH_UNIX table (codec.hip use_lens; 0x20000 keeps
@@ -325,8 +323,7 @@ def test_emit_from_plan_lengths(R, oracle, monkeypatch, variant, given_len):
     one 1M-record plan chunk — bytes, offsets and statuses equal to the
     oracle's."""
     import torch
-    monkeypatch.setenv("ONC_RPC_VARIANT", str(variant))
-    codec = R.Codec(0)
+    codec = R.Codec(0, variant=variant)
     try:
         for hb in (S.cpu_roundtrip(3000, seed=51), S.mixed(3000, seed=52, pmin=0, pmax=90, exotic=0.3),
                    S.call_unix16(1_050_000, 20, seed=53)):
@@ -357,9 +354,9 @@ def test_emit_from_plan_lengths(R, oracle, monkeypatch, variant, given_len):
 
 
 @pytest.mark.parametrize("variant", [0, 0x200, 0x400])
-def test_small_encode_chunks(R, oracle, monkeypatch, variant):
+def test_small_encode_chunks(R, oracle, variant):
     """The chunked encode (codec.hip encode_batch) with 2048-record chunks
-    (ONC_RPC_ENC_CHUNK), so that small batches cross many chunk boundaries:
+    (onc_codec_options.enc_chunk), so that small batches cross many chunk boundaries:
     RpcMessage batches of every shape (mixed with failing records and odd
     payloads, AUTH_UNIX-heavy with the plan's lengths read by the emit) at an
     odd writer position with the capacity ending inside a later chunk, on the
@@ -368,9 +365,7 @@ def test_small_encode_chunks(R, oracle, monkeypatch, variant):
     to the oracle's whole-batch loop."""
     import torch
     from test_body_roots import ROOTS, _valid_messages
-    monkeypatch.setenv("ONC_RPC_ENC_CHUNK", "2048")
-    monkeypatch.setenv("ONC_RPC_VARIANT", str(variant))
-    codec = R.Codec(0)
+    codec = R.Codec(0, variant=variant, enc_chunk=2048)
     try:
         for hb in (S.mixed(9001, seed=61, pmin=0, pmax=300, exotic=0.2), S.cpu_roundtrip(7000, seed=62),
                    S.call_none(5000, 256, seed=63)):

@@ -33,9 +33,42 @@ def test_library_exports_every_header_symbol():
     import onc_rpc_amd.runtime as R
     assert sorted(R.EXPORTED) == funcs
     lib.onc_abi_version.restype = C.c_int
-    assert lib.onc_abi_version() == R.ABI_VERSION == 5
+    assert lib.onc_abi_version() == R.ABI_VERSION == 6
     lib.onc_status_str.restype = C.c_char_p
     assert lib.onc_status_str(1) == b"incomplete rpc message"
+
+
+def test_library_reads_no_environment():
+    """ABI 6: kernel choices, chunk sizes and the decode policy are explicit
+    onc_codec_options; the shipping library names no environment variable
+    (a stray one in a server process cannot change what it runs)."""
+    blob = open(LIB, "rb").read()
+    assert b"ONC_RPC_" not in blob
+    assert b"getenv" not in blob
+
+
+def test_codec_options_layout_matches_header():
+    import onc_rpc_amd.runtime as R
+    prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "onc_rpc.h"
+int main(void){
+ printf("%zu %zu %zu %zu %zu %zu\n", sizeof(onc_codec_options), offsetof(onc_codec_options, flags),
+        offsetof(onc_codec_options, decode_policy), offsetof(onc_codec_options, variant),
+        offsetof(onc_codec_options, enc_chunk), offsetof(onc_codec_options, frame_chunk));
+ return 0;
+}
+'''
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "o.c")
+        open(src, "w").write(prog)
+        exe = os.path.join(d, "o")
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), src, "-o", exe])
+        got = [int(x) for x in subprocess.check_output([exe]).split()]
+    O = R.OncCodecOptions
+    assert got == [C.sizeof(O), O.flags.offset, O.decode_policy.offset, O.variant.offset, O.enc_chunk.offset,
+                   O.frame_chunk.offset]
 
 
 def test_library_is_gfx950_code_object():
