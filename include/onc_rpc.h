@@ -52,7 +52,9 @@ extern "C" {
  * 6: onc_codec_create_ex + onc_codec_options (kernel choices, chunk sizes and
  *    the decode policy are explicit options; the library reads no
  *    environment variable), onc_codec_set_decode_policy, calls refuse to grow
- *    scratch while the stream is being captured (ONC_RC_ECAPTURE). */
+ *    scratch while the stream is being captured (ONC_RC_ECAPTURE); an
+ *    AUTH_UNIX onc_auth carries its declared serialised length (kind_len
+ *    bits 0..23, written by the decoder; 0 = not declared). */
 #define ONC_RPC_ABI_VERSION 6
 
 /* ------------------------------------------------------------------------ */
@@ -205,7 +207,23 @@ extern "C" {
  *  id       : wire flavor discriminant. Encode writes 0/1/2 for kinds
  *             NONE/UNIX/SHORT and `id` for UNKNOWN; decode stores the value read.
  *  kind_len : bits 0..23 opaque body length (NONE/SHORT/UNKNOWN),
- *             bits 24..31 ONC_KIND_*. Unused length bits are 0 for UNIX.
+ *             bits 24..31 ONC_KIND_*.
+ *             UNIX (ABI 6): the declared length — AuthUnixParams::serialised_len
+ *             (unix_params.rs:219-230: 20 + 4 * ceil(name_len / 4) + 4 * ngids)
+ *             — or 0 (not declared). The decoder always declares it. On
+ *             encode a declared length lets the length pass (onc_encode,
+ *             onc_encode_plan) size the record from the descriptor alone,
+ *             without reading the 96-byte parameter block; the emit checks
+ *             the block when it serialises it (the AuthUnixParams::new / Gids
+ *             panics, the machine name inside the auth arena, and declared ==
+ *             serialised length — a mismatch is ONC_ENC_BAD_DESCRIPTOR).
+ *             Statuses are the reference order's either way. One placement
+ *             difference: a record whose only failure is such a block check
+ *             keeps the extent its descriptor declares in the output, its
+ *             header bytes zero and its payload in place (every other failing
+ *             record takes 0 bytes). onc_encode_lengths, onc_encode_iov and
+ *             the body roots check every block up front (failing records:
+ *             length 0).
  *  ref      : NONE/SHORT/UNKNOWN: byte offset of the body in the auth arena
  *             (decode: in the wire buffer). UNIX: index into the unix table. */
 typedef struct onc_auth {
@@ -446,7 +464,8 @@ int onc_encode(onc_codec* codec, const onc_batch* batch,
  *                     arguments and results as onc_encode.
  * The plan belongs to the handle: emit must name the batch last planned on
  * it (same msgs pointer and n) with the status array the plan filled (the
- * plan's statuses stand, emit only adds ONC_ENC_WRITE_ZERO), else
+ * plan's statuses stand; emit adds ONC_ENC_WRITE_ZERO and the status of a
+ * declared AUTH_UNIX auth's parameter-block check, onc_auth), else
  * ONC_RC_EINVAL; any other call on the handle in between that uses its
  * scratch (every encode, decode_lengths and scan_lengths call) discards the
  * plan (then ONC_RC_EINVAL too). The descriptors must not change in between,

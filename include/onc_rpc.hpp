@@ -657,7 +657,13 @@ inline void BatchEncoder::put_auth(const AuthFlavor& a, onc_auth& d) {
             u.name_off = auth_.size();
             u.name_len = uint32_t(p.machine_name().len);
             auth_.insert(auth_.end(), p.machine_name().ptr, p.machine_name().ptr + p.machine_name().len);
-            d.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
+            // ABI 6: declare serialised_len (unix_params.rs:219-230) so that the
+            // encoder's length pass reads no parameter block; a block that
+            // would panic is left undeclared (0: every check up front)
+            const uint32_t ng = u.ngids, nl = u.name_len;
+            d.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, nl <= ONC_MAX_MACHINE_NAME_LEN && ng <= ONC_MAX_GIDS
+                                                          ? 20u + 4u * ((nl + 3u) / 4u) + 4u * ng
+                                                          : 0u);
             d.ref = unix_.size();
             unix_.push_back(u);
             return;

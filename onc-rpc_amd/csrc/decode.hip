@@ -150,7 +150,7 @@ __device__ __forceinline__ int32_t auth_slice(const Rd& R, uint32_t& pos, uint32
         pos += 4u * ng;
         if (pos - start != n) return ONC_ERR_INVALID_AUTH_DATA;          // unix_params.rs:117-119
         put_unix(us, slot, stamp, uid, gid, ng, rec_off + name_pos, nl, gids);
-        a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
+        a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, n);     // ABI 6: the declared length (= serialised_len)
         a.ref = slot;
         return ONC_OK;
     }
@@ -206,7 +206,7 @@ __device__ __forceinline__ int32_t auth_bytes(const Rd& R, uint32_t& pos, uint32
         // params.serialised_len() != auth_data.len() -> InvalidAuthData (flavor.rs:204-208)
         if (20u + nl + pad4(nl) + 4u * ng != n) return ONC_ERR_INVALID_AUTH_DATA;
         put_unix(us, slot, stamp, uid, gid, ng, rec_off + name_pos, nl, gids);
-        a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
+        a.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, n);     // ABI 6: the declared length (= serialised_len)
         a.ref = slot;
         return ONC_OK;
     }
@@ -375,7 +375,7 @@ __device__ __forceinline__ int32_t parse_root(const Rd& R, uint32_t end, uint64_
         } else if (root == ONC_ROOT_AUTH_UNIX_PARAMS) {
             st = unix_params_root<MODE>(R, pos, end, rec_off, 2 * i, param, us);
             m.cred.id = ONC_AUTH_UNIX;
-            m.cred.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
+            m.cred.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, pos);   // serialised_len (cursor from 0)
             m.cred.ref = 2 * i;
         } else {                                               // opaque.rs:72-98 / bytes_ext.rs:25-42
             const uint32_t max_len = min(param, ONC_OPAQUE_MAX_LEN);

@@ -107,10 +107,17 @@ class HostBatch:
         return len(self.msgs)
 
 
-def build_batch(messages):
+def unix_body_len(name_len, ngids):
+    """AuthUnixParams::serialised_len (unix_params.rs:219-230)."""
+    return 20 + 4 * ((name_len + 3) // 4) + 4 * ngids
+
+
+def build_batch(messages, declare=True):
     """message dicts -> HostBatch (construction of the reference values;
     limits are NOT enforced here so that the codec's panic statuses can be
-    exercised)."""
+    exercised). declare: AUTH_UNIX auths within the limits carry their
+    serialised length in onc_auth.len (ABI 6; the encoder's length pass then
+    reads no parameter block); False leaves every one 0 (undeclared)."""
     n = len(messages)
     msgs = np.zeros(n, MSG_DTYPE)
     unix_rows = []
@@ -130,7 +137,9 @@ def build_batch(messages):
             g = list(a["gids"])[:16]
             row["gids"][: len(g)] = g
             auth.extend(name)
-            msgs[prefix + "_kind_len"][i] = pack_kind_len(KIND_UNIX, 0)
+            ok = len(name) <= 255 and len(a["gids"]) <= 16
+            msgs[prefix + "_kind_len"][i] = pack_kind_len(
+                KIND_UNIX, unix_body_len(len(name), len(a["gids"])) if declare and ok else 0)
             msgs[prefix + "_ref"][i] = len(unix_rows)
             unix_rows.append(row)
         else:

@@ -51,7 +51,7 @@ def call_unix16(n, payload_len=1024, seed=3, stamp_from_index=True, xid=None, pr
     msgs["payload_len"] = payload_len
     msgs["payload_off"] = np.arange(n, dtype=np.uint64) * np.uint64(payload_len)
     msgs["cred_id"] = 1
-    msgs["cred_kind_len"] = int(L.pack_kind_len(L.KIND_UNIX, 0))
+    msgs["cred_kind_len"] = int(L.pack_kind_len(L.KIND_UNIX, L.unix_body_len(0, 16)))   # declared (ABI 6)
     msgs["cred_ref"] = np.arange(n, dtype=np.uint64)
     msgs["verf_kind_len"] = NONE_NONE
     unix = np.zeros(n, L.UNIX_DTYPE)
@@ -131,7 +131,11 @@ def mixed(n, seed=2, pmin=64, pmax=4096, exotic=0.0):
     msgs["cred_kind_len"] = NONE_NONE
     msgs["verf_kind_len"] = NONE_NONE
     msgs["cred_id"] = np.where(unix_cred, 1, 0)
-    msgs["cred_kind_len"][unix_cred] = int(L.pack_kind_len(L.KIND_UNIX, 0))
+    # three in four AUTH_UNIX credentials declare their serialised length
+    # (ABI 6), the rest leave it 0: both planning paths in one batch
+    decl = rng.random(n_unix) < 0.75
+    blen = np.where(decl, 20 + 4 * ((name_len.astype(np.int64) + 3) // 4) + 4 * ng.astype(np.int64), 0)
+    msgs["cred_kind_len"][unix_cred] = (np.uint32(L.KIND_UNIX) << np.uint32(24)) | blen.astype(np.uint32)
     msgs["cred_ref"][unix_cred] = np.arange(n_unix, dtype=np.uint64)
 
     if exotic > 0:

@@ -404,6 +404,9 @@ static o_err auth_from_desc(const onc_auth* d, const onc_unix_params* unix_table
         a->unix.gid = p->gid;
         a->unix.ngids = p->ngids;
         memcpy(a->unix.gids, p->gids, sizeof(uint32_t) * p->ngids);
+        /* ABI 6 (include/onc_rpc.h onc_auth): a declared length must be the
+         * block's serialised_len (a descriptor the Rust types cannot hold) */
+        if (len != 0 && len != unix_serialised_len(&a->unix)) return o_error(ONC_ENC_BAD_DESCRIPTOR, 0, 0);
         return O_OK;
     }
     a->id = d->id;
@@ -473,7 +476,8 @@ static void auth_to_desc(const o_auth* a, const uint8_t* base, uint64_t slot, on
     memset(d, 0, sizeof(*d));
     d->id = a->kind == O_AUTH_UNKNOWN ? a->id : (uint32_t)a->kind;
     if (a->kind == O_AUTH_UNIX) {
-        d->kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
+        /* ABI 6: the decoded credential declares its serialised length */
+        d->kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, (uint32_t)unix_serialised_len(&a->unix));
         d->ref = slot;
         memset(u, 0, sizeof(*u));
         u->stamp = a->unix.stamp;
@@ -922,6 +926,56 @@ int32_t oracle_encode_message(const onc_msg* msg, const onc_unix_params* unix_ta
     return e.code;
 }
 
+/* The library's placement of a record whose AUTH_UNIX auths declare their
+ * length (include/onc_rpc.h onc_auth, ABI 6 — the library's own contract,
+ * not a reference behaviour): its length pass plans every declared auth from
+ * the descriptor alone and checks the parameter blocks only while writing.
+ * So a record that fails only a block check (a panic of AuthUnixParams::new /
+ * Gids, or declared != serialised length) still takes the extent the
+ * descriptor declares: its header bytes zero, its payload (a Call's, an
+ * accepted Success's) in place. Returns 1 with that extent and header size
+ * when every descriptor-only check passes (encode.hip plan_record<true>). */
+static int declared_extent(const onc_msg* d, const onc_unix_params* unix_table, uint64_t* len, uint64_t* hdr) {
+    /* one auth: serialised_len (id + body) and associated_data_len bound */
+    uint64_t aw[2] = {0, 0}, assoc[2] = {0, 0};
+    const onc_auth* auths[2] = {&d->cred, &d->verf};
+    const int call = d->msg_type == ONC_MSG_CALL;
+    const int acc = d->msg_type == ONC_MSG_REPLY && d->reply_stat == ONC_REPLY_ACCEPTED;
+    if (!call && !acc) return 0;                      /* no AUTH_UNIX auth: nothing deferred */
+    if (acc && d->stat > ONC_ACCEPT_SYSTEM_ERR) return 0;
+    for (int k = call ? 0 : 1; k < 2; k++) {
+        const onc_auth* a = auths[k];
+        const uint32_t kind = ONC_AUTH_KIND(*a), l = ONC_AUTH_LEN(*a);
+        if (kind > ONC_KIND_UNKNOWN) return 0;
+        if (kind == ONC_KIND_UNIX && l != 0) {
+            if (l < 20 || (l & 3) || l > 20 + 4 * 64 + 4 * 16) return 0;   /* implausible */
+            aw[k] = 8 + l;
+            assoc[k] = l - 8;                         /* > 200 exactly when the true value is */
+        } else if (kind == ONC_KIND_UNIX) {
+            const onc_unix_params* p = &unix_table[a->ref];
+            if (p->name_len > ONC_MAX_MACHINE_NAME_LEN || p->ngids > ONC_MAX_GIDS) return 0;
+            aw[k] = 8 + 20 + 4 * ((p->name_len + 3) / 4) + 4ull * p->ngids;
+            assoc[k] = 12 + p->name_len + 4ull * p->ngids;
+        } else {
+            aw[k] = 8 + l + oracle_pad_length(l);
+            assoc[k] = l;
+        }
+    }
+    uint64_t h, body;
+    if (call) {
+        h = 28 + aw[0] + aw[1];
+        body = d->payload_len;
+    } else {
+        h = 16 + aw[1] + 4 + (d->stat == ONC_ACCEPT_PROG_MISMATCH ? 8 : 0);
+        body = d->stat == ONC_ACCEPT_SUCCESS ? d->payload_len : 0;
+    }
+    if ((h + body) & 0xFFFFFFFF80000000ull) return 0;
+    if (assoc[0] > ONC_MAX_AUTH_LEN || assoc[1] > ONC_MAX_AUTH_LEN) return 0;
+    *len = h + body;
+    *hdr = h;
+    return 1;
+}
+
 void oracle_encode_batch(uint64_t n, const onc_msg* msgs, const onc_unix_params* unix_table,
                          const uint8_t* auth_arena, const uint8_t* payload_arena,
                          uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
@@ -933,6 +987,14 @@ void oracle_encode_batch(uint64_t n, const onc_msg* msgs, const onc_unix_params*
         int32_t st = oracle_encode_message(&msgs[i], unix_table, auth_arena, payload_arena,
                                            cap ? out + off : out, cap, &written, &slen);
         uint64_t len = (st == ONC_OK || st == ONC_ENC_WRITE_ZERO) ? slen : 0;
+        uint64_t dlen, dhdr;
+        if (len == 0 && st != ONC_OK && declared_extent(&msgs[i], unix_table, &dlen, &dhdr)) {
+            /* failed a deferred block check only: the declared extent, header zero, payload copied */
+            len = dlen;
+            const onc_msg* d = &msgs[i];
+            for (uint64_t b = 0; b < dlen && b < cap; b++)
+                out[off + b] = b < dhdr ? 0 : payload_arena[d->payload_off + (b - dhdr)];
+        }
         if (rec_off) rec_off[i] = off;
         if (status) status[i] = st;
         if (rec_len) rec_len[i] = (uint32_t)len;

@@ -419,3 +419,56 @@ def test_gpu_body_short_headers_every_alignment(codec, R, oracle, root):
         assert np.array_equal(off.cpu().numpy().view(np.uint64), o_off)
         assert b[shift:shift + total].tobytes() == o_wire, (L.ROOT_NAMES[root], shift)
         assert (b[:shift] == 0xA5).all() and (b[shift + total:] == 0xA5).all()
+
+
+def _too_long_batch():
+    """CallBody / RpcMessage records around the 2^31 limit: a Call with
+    AuthNone(None) credential and verifier has a 32-byte CallBody header
+    (call_body.rs:111-119) and a 44-byte RpcMessage (+ mark, xid, type);
+    payload lengths put each root's total at 2^31 - 1 and 2^31. Lengths only:
+    the payload is never read (a 16-byte arena declared as 4 GiB)."""
+    msgs = np.zeros(4, L.MSG_DTYPE)
+    msgs["msg_type"] = L.MSG_CALL
+    msgs["payload_len"] = [(1 << 31) - 33, (1 << 31) - 32, (1 << 31) - 45, (1 << 31) - 44]
+    return L.HostBatch(msgs, np.zeros(1, L.UNIX_DTYPE), np.zeros(16, np.uint8), np.zeros(16, np.uint8))
+
+
+def test_oracle_too_long_boundary(oracle):
+    """The 2^31 limit at its boundary. RpcMessage::serialise_into refuses a
+    record of 2^31 bytes or more (rpc_message.rs:146-151: the record mark's
+    length field). The body roots apply the same limit: a deliberate
+    deviation (DESIGN.md §7) — the reference's CallBody::serialise_into has no
+    limit and its serialised_len is a u32 — so that any body also frames as a
+    message; parity unpinned, no reference test covers it."""
+    import ctypes as C
+    hb = _too_long_batch()
+    lib = oracle.load()
+    for root, ok, bad in ((L.ROOT_CALL_BODY, 0, 1), (L.ROOT_RPC_MESSAGE, 2, 3)):
+        off = np.zeros(5, np.uint64)
+        st = np.zeros(4, np.int32)
+        ln = np.zeros(4, np.uint32)
+        lib.oracle_encode_body_batch(root, 4, C.c_void_p(hb.msgs.ctypes.data), C.c_void_p(hb.unix.ctypes.data),
+                                     C.c_void_p(hb.auth_arena.ctypes.data), C.c_void_p(hb.payload_arena.ctypes.data),
+                                     None, 0, C.c_void_p(off.ctypes.data), C.c_void_p(st.ctypes.data),
+                                     C.c_void_p(ln.ctypes.data))
+        assert st[ok] == 105 and ln[ok] == (1 << 31) - 1          # fits (WRITE_ZERO: no capacity given)
+        assert st[bad] == 100 and ln[bad] == 0                    # ONC_ENC_TOO_LONG
+
+
+@pytest.mark.gpu
+def test_gpu_too_long_boundary(codec, R):
+    """onc_encode_body_lengths / onc_encode_lengths at the same boundary as
+    the oracle test: 2^31 - 1 fits, 2^31 is ONC_ENC_TOO_LONG, for the
+    CallBody root and for RpcMessage."""
+    import torch
+    hb = _too_long_batch()
+    db = R.DeviceBatch.from_host(hb)
+    db.payload_len = 1 << 32
+    rl = torch.empty(4, dtype=torch.int32, device="cuda")
+    st = torch.empty(4, dtype=torch.int32, device="cuda")
+    for root, ok, bad in ((L.ROOT_CALL_BODY, 0, 1), (L.ROOT_RPC_MESSAGE, 2, 3)):
+        codec.encode_body_lengths(root, db, rl, st)
+        codec.sync()
+        s, n = st.cpu().numpy(), rl.cpu().numpy().view(np.uint32)
+        assert s[ok] == 0 and n[ok] == (1 << 31) - 1
+        assert s[bad] == 100 and n[bad] == 0

@@ -148,3 +148,130 @@ def test_maximal_auth_unix(codec, R, oracle):
     hb = L.build_batch(msgs)
     _check(R, codec, oracle, hb)
     _check(R, codec, oracle, hb, shift=13)
+
+
+# ---------------------------------------------------------------------------
+# Declared AUTH_UNIX lengths (ABI 6, include/onc_rpc.h onc_auth): the length
+# pass plans a declared auth from the descriptor alone and the emit runs the
+# parameter-block checks it deferred.
+# ---------------------------------------------------------------------------
+def _enc_oracle_sized(R, codec, hb, oracle, shift=0, cap=None, fill=0x5A):
+    import torch
+    o_wire, o_off, o_st, o_len = oracle.encode_batch(hb) if cap is None else oracle.encode_batch(hb, out_cap=cap)
+    total = int(o_off[hb.n])
+    cap = total if cap is None else cap
+    db = R.DeviceBatch.from_host(hb)
+    buf = torch.full((shift + max(cap, total) + 64,), fill, dtype=torch.uint8, device="cuda")
+    rec_off = torch.empty(hb.n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(max(hb.n, 1), dtype=torch.int32, device="cuda")
+    rl = torch.empty(max(hb.n, 1), dtype=torch.int32, device="cuda")
+    codec.encode(db, buf[shift:], rec_off, st, rl, out_cap=cap)
+    codec.sync()
+    b = buf.cpu().numpy()
+    assert np.array_equal(st.cpu().numpy()[:hb.n], o_st), \
+        f"status {np.nonzero(st.cpu().numpy()[:hb.n] != o_st)[0][:8]}"
+    assert np.array_equal(rec_off.cpu().numpy().view(np.uint64), o_off)
+    assert np.array_equal(rl.cpu().numpy().view(np.uint32)[:hb.n], o_len)
+    assert b[shift:shift + len(o_wire)].tobytes() == o_wire
+    assert (b[:shift] == fill).all() and (b[shift + cap:] == fill).all()
+    return o_st, o_len
+
+
+def _adversarial(seed, n=3000):
+    """random_messages with declared lengths, then a quarter of the AUTH_UNIX
+    auths (credentials and verifiers, Calls and accepted replies) broken:
+    declared != serialised (+4 / -4), a 300-byte machine name or 17 gids in
+    the block (panics) under a plausible declared length, an implausible
+    declared length (3, 18, 400: planned in full), or a block failure next to
+    a failing descriptor-only check (a 201-byte opaque verifier: the full
+    plan's reference-order status)."""
+    rng = np.random.default_rng(seed)
+    hb = L.build_batch(S.random_messages(n, seed=seed, max_payload=300))
+    m, u = hb.msgs, hb.unix
+    for f in ("cred", "verf"):
+        isu = ((m[f + "_kind_len"] >> 24) == L.KIND_UNIX) & (m[f + "_kind_len"] & 0xFFFFFF != 0)
+        for i in np.nonzero(isu)[0]:
+            c = int(rng.integers(0, 8))
+            ref = int(m[f + "_ref"][i])
+            ln = int(m[f + "_kind_len"][i] & 0xFFFFFF)
+            if c == 0:
+                m[f + "_kind_len"][i] = int(L.pack_kind_len(L.KIND_UNIX, ln + 4))
+            elif c == 1 and ln >= 24:
+                m[f + "_kind_len"][i] = int(L.pack_kind_len(L.KIND_UNIX, ln - 4))
+            elif c == 2:
+                u["name_len"][ref] = 300
+            elif c == 3:
+                u["ngids"][ref] = 17
+            elif c == 4:
+                m[f + "_kind_len"][i] = int(L.pack_kind_len(L.KIND_UNIX, int(rng.choice([3, 18, 400]))))
+            elif c == 5 and m["msg_type"][i] == L.MSG_CALL and f == "cred":
+                u["ngids"][ref] = 17
+                m["verf_kind_len"][i] = int(L.pack_kind_len(L.KIND_SHORT, 201))
+                m["verf_ref"][i] = 0
+    return hb
+
+
+@pytest.mark.parametrize("seed", [71, 72])
+def test_declared_lengths_broken_blocks(codec, R, oracle, seed):
+    """Records whose only failure is a deferred block check keep the extent
+    their descriptor declares (header bytes zero, payload in place) with the
+    check's status; the others get the full plan's reference-order status
+    and no bytes — the oracle's restatement of the rule, bit-exact, at two
+    writer positions and with a capacity inside the batch. onc_encode_lengths
+    checks every block up front (failing records: length 0)."""
+    import torch
+    hb = _adversarial(seed)
+    o_st, o_len = _enc_oracle_sized(R, codec, hb, oracle)
+    assert (o_st != 0).sum() > 200 and ((o_st != 0) & (o_len != 0)).sum() > 100   # both kinds of failure
+    _enc_oracle_sized(R, codec, hb, oracle, shift=7)
+    total = int(o_len.astype(np.int64).sum())
+    _enc_oracle_sized(R, codec, hb, oracle, shift=3, cap=total // 2 + 5)
+    db = R.DeviceBatch.from_host(hb)
+    rl = torch.empty(hb.n, dtype=torch.int32, device="cuda")
+    st = torch.empty(hb.n, dtype=torch.int32, device="cuda")
+    codec.encode_lengths(db, rl, st)
+    codec.sync()
+    assert np.array_equal(st.cpu().numpy(), o_st)
+    assert np.array_equal(rl.cpu().numpy().view(np.uint32), np.where(o_st == 0, o_len, 0))
+
+
+def test_declared_equals_undeclared(codec, R, oracle):
+    """The same messages with every AUTH_UNIX length declared and with none:
+    identical wire, offsets and statuses (and the oracle's)."""
+    msgs = S.random_messages(4000, seed=73, max_payload=500)
+    a = _enc_oracle_sized(R, codec, L.build_batch(msgs, declare=True), oracle, shift=1)
+    b = _enc_oracle_sized(R, codec, L.build_batch(msgs, declare=False), oracle, shift=1)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    ow_a = oracle.encode_batch(L.build_batch(msgs, declare=True))[0]
+    ow_b = oracle.encode_batch(L.build_batch(msgs, declare=False))[0]
+    assert ow_a == ow_b
+
+
+def test_declared_name_outside_arena(codec, R, oracle):
+    """A declared credential whose machine name lies outside the auth arena
+    (the GPU's bounds check, which the oracle does not model): BAD_DESCRIPTOR
+    with the declared extent — the same bytes and offsets as the oracle's for
+    the same record failing another deferred check (17 gids)."""
+    hb = S.call_unix16(2000, 40, seed=74)
+    hb.unix["name_len"][100:110] = 8        # declared lengths follow the names
+    hb.msgs["cred_kind_len"][100:110] = int(L.pack_kind_len(L.KIND_UNIX, L.unix_body_len(8, 16)))
+    hb.auth_arena = np.zeros(64, np.uint8)
+    hb.unix["name_off"][100:110] = 16
+    ref = L.HostBatch(hb.msgs.copy(), hb.unix.copy(), hb.auth_arena, hb.payload_arena)
+    ref.unix["ngids"][[103, 107]] = 17
+    hb.unix["name_off"][[103, 107]] = 1 << 40
+    import torch
+    o_wire, o_off, o_st, o_len = oracle.encode_batch(ref)
+    db = R.DeviceBatch.from_host(hb)
+    total = int(o_off[hb.n])
+    buf = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
+    off = torch.empty(hb.n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(hb.n, dtype=torch.int32, device="cuda")
+    codec.encode(db, buf, off, st, out_cap=total)
+    codec.sync()
+    g_st = st.cpu().numpy()
+    want = o_st.copy()
+    want[[103, 107]] = 104                  # ONC_ENC_BAD_DESCRIPTOR
+    assert np.array_equal(g_st, want)
+    assert np.array_equal(off.cpu().numpy().view(np.uint64), o_off)
+    assert buf.cpu().numpy()[:total].tobytes() == o_wire
