@@ -221,9 +221,10 @@ extern "C" {
  *             difference: a record whose only failure is such a block check
  *             keeps the extent its descriptor declares in the output, its
  *             header bytes zero and its payload in place (every other failing
- *             record takes 0 bytes). onc_encode_lengths, onc_encode_iov and
- *             the body roots check every block up front (failing records:
- *             length 0).
+ *             record takes 0 bytes). onc_encode_lengths reports the same
+ *             extents (with every check's status) and onc_encode_iov places
+ *             records by them (such a record: no header bytes, zero iovec
+ *             lengths); the body roots check every block up front.
  *  ref      : NONE/SHORT/UNKNOWN: byte offset of the body in the auth arena
  *             (decode: in the wire buffer). UNIX: index into the unix table. */
 typedef struct onc_auth {
@@ -353,6 +354,7 @@ typedef struct onc_codec onc_codec;
 #define ONC_VARIANT_WS_PIPELINE      0x10000u  /* wave-specialised: the pipeline on header-heavy batches too */
 #define ONC_VARIANT_EMIT_REPLAN      0x20000u  /* wave-per-tile enc_emit re-plans instead of reading the plan's lengths */
 #define ONC_VARIANT_WHOLE_PLAN       0x40000u  /* plan a large batch whole instead of in chunks */
+#define ONC_VARIANT_EMIT_PRELOAD     0x80000u  /* wave-per-tile enc_emit: preload the AUTH_UNIX credential block (lab) */
 
 #define ONC_OPT_FORCE_SCAN 0x1u   /* always launch the separate block-scan kernels (tests of that path) */
 
@@ -431,8 +433,11 @@ const char* onc_kernel_name(int kernel_id);
 
 /* serialised_len() of every record (src/rpc_message.rs:201-204) plus the
  * encode-time validation of serialise_into (oversize, panics).
- * rec_len[dev,n] receives the length (0 for a record whose status != OK);
- * status[dev,n] receives ONC_OK or an ONC_ENC_* code. */
+ * rec_len[dev,n] receives the length (0 for a record whose status != OK,
+ * except a declared AUTH_UNIX record failing only a parameter-block check:
+ * its declared extent, as onc_encode places it — onc_auth), so the sum is
+ * the size of onc_encode's output; status[dev,n] receives ONC_OK or an
+ * ONC_ENC_* code. */
 int onc_encode_lengths(onc_codec* codec, const onc_batch* batch,
                        uint32_t* rec_len, int32_t* status);
 

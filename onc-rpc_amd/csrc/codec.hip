@@ -404,6 +404,7 @@ int onc_encode_lengths(onc_codec* c, const onc_batch* batch, uint32_t* rec_len, 
     a.bounds = bounds_of(batch);
     a.status = status;
     a.rec_len = rec_len;
+    a.decl = 2;        // the extents onc_encode places, every check up front (onc_auth)
     bind_scratch(c, a);
     forget_plan(c);
     return run(c, ONC_K_ENC_LEN, "enc_len", [&] { return onc::launch_enc_len(a, c->stream); });

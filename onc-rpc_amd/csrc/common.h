@@ -202,8 +202,9 @@ __device__ __forceinline__ uint32_t meta_hw(uint32_t m) { return m >> 16; }
 // serialise_into in reference order: descriptor / construction panics
 // (cred, then verf), oversize (rpc_message.rs:146-151), then the
 // associated-data assert (flavor.rs:110, cred before verf).
-// kDecl: declared AUTH_UNIX lengths are taken as given (plan_auth); a record
-// that fails this form fails the full one too, with the full one's status.
+// kDecl: a Call credential's declared AUTH_UNIX length is taken as given
+// (plan_auth); a record that fails this form fails the full one too, with
+// the full one's status.
 template <bool kDecl = false>
 __device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_params* unix, const Bounds& bd) {
     RecPlan r;
@@ -214,9 +215,11 @@ __device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_
     uint64_t body = 0;
     uint32_t assoc_c = 0, assoc_v = 0;
     if (d.msg_type == ONC_MSG_CALL) {
+        // (only a Call's credential is planned from its declared length: a
+        // verifier's block is checked here — AUTH_UNIX verifiers are rare)
         AuthPlan c = plan_auth<kDecl>(d.cred, unix, bd);
         if (c.status) { r.status = c.status; return r; }
-        AuthPlan v = plan_auth<kDecl>(d.verf, unix, bd);
+        AuthPlan v = plan_auth<false>(d.verf, unix, bd);
         if (v.status) { r.status = v.status; return r; }
         cw = c.words; vw = v.words;
         assoc_c = c.assoc; assoc_v = v.assoc;
@@ -225,7 +228,7 @@ __device__ __forceinline__ RecPlan plan_record(const onc_msg& d, const onc_unix_
     } else if (d.msg_type == ONC_MSG_REPLY) {
         if (d.reply_stat == ONC_REPLY_ACCEPTED) {
             if (d.stat > ONC_ACCEPT_SYSTEM_ERR) { r.status = ONC_ENC_BAD_DESCRIPTOR; return r; }
-            AuthPlan v = plan_auth<kDecl>(d.verf, unix, bd);
+            AuthPlan v = plan_auth<false>(d.verf, unix, bd);
             if (v.status) { r.status = v.status; return r; }
             vw = v.words; assoc_v = v.assoc;
             // mark, xid, mtype, reply_stat, verf, accept_stat [, low, high]
@@ -267,12 +270,12 @@ __device__ __forceinline__ int32_t check_declared_unix(const u32x4& q0, const u3
     return ONC_OK;
 }
 
-// The emit's side of plan_record<true>: the first failing deferred check of
-// a record's declared AUTH_UNIX auths (credential before verifier), run by
-// put_unix_words on the block words it loads anyway.
+// The emit's side of plan_record<true>: the deferred checks of a Call's
+// declared AUTH_UNIX credential, run by put_unix_words on the block words it
+// loads anyway (emits that did not preload the block).
 struct DeclCheck {
     uint64_t auth_len;   // the auth arena's size (the machine name's bounds)
-    int32_t st;
+    int32_t* st;         // receives the failing check's status (left alone when the block passes)
 };
 
 struct EncSrc {
@@ -331,16 +334,20 @@ template <bool kLen, class Sink>
 __device__ __forceinline__ void put_unix_words(const UnixRegs& u, const EncSrc& s, Sink& out,
                                                DeclCheck* dc = nullptr, uint32_t declared = 0) {
     const u32x4* q = u.q;
+    uint32_t ng = q[0].w, nl = q[1].z;
     if (dc && declared != 0) {
-        // a block that fails is not serialised: the record stops here, never
-        // past the declared extent its placement has (nothing written so far
-        // exceeds it)
-        if (dc->st == ONC_OK) dc->st = check_declared_unix(q[0], q[1], declared, dc->auth_len);
-        if (dc->st != ONC_OK) return;
+        // a block that fails is serialised as an empty one (no name read, no
+        // gids: 20 bytes, never past the declared extent, which is >= 20);
+        // its status goes to *dc->st and the caller clears what the record
+        // wrote
+        const int32_t st = check_declared_unix(q[0], q[1], declared, dc->auth_len);
+        if (st != ONC_OK) {
+            *dc->st = st;
+            ng = nl = 0;
+        }
     }
-    const uint32_t stamp = q[0].x, uid = q[0].y, gid = q[0].z, ng = q[0].w;
+    const uint32_t stamp = q[0].x, uid = q[0].y, gid = q[0].z;
     const uint64_t name_off = uint64_t(q[1].x) | (uint64_t(q[1].y) << 32);
-    const uint32_t nl = q[1].z;
     const uint32_t gids[ONC_MAX_GIDS] = {q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w,
                                          q[4].x, q[4].y, q[4].z, q[4].w, q[5].x, q[5].y, q[5].z, q[5].w};
     if (kLen) out(bswap(20u + 4u * words4(nl) + 4u * ng));
@@ -401,8 +408,7 @@ __device__ __forceinline__ void put_call_words(const onc_msg& d, const EncSrc& s
     out(bswap(d.u.call.program_version));
     out(bswap(d.u.call.procedure));
     put_auth_words(d.cred, s, out, cred_pre, use_pre, dc);
-    if (dc && dc->st != ONC_OK) return;
-    put_auth_words(d.verf, s, out, nullptr, false, dc);
+    put_auth_words(d.verf, s, out);
 }
 
 // AcceptedStatus::serialise_into (accepted_reply.rs:195-211) up to a
@@ -431,12 +437,10 @@ __device__ __forceinline__ void put_rejected_words(const onc_msg& d, Sink& out) 
 // ReplyBody::serialise_into (reply_body.rs:45-56; AcceptedReply
 // accepted_reply.rs:58-61) up to a Success payload.
 template <class Sink>
-__device__ __forceinline__ void put_reply_words(const onc_msg& d, const EncSrc& s, Sink& out,
-                                                DeclCheck* dc = nullptr) {
+__device__ __forceinline__ void put_reply_words(const onc_msg& d, const EncSrc& s, Sink& out) {
     out(bswap(uint32_t(d.reply_stat)));
     if (d.reply_stat == ONC_REPLY_ACCEPTED) {
-        put_auth_words(d.verf, s, out, nullptr, false, dc);
-        if (dc && dc->st != ONC_OK) return;
+        put_auth_words(d.verf, s, out);
         put_accepted_status_words(d, out);
         return;
     }
@@ -446,7 +450,7 @@ __device__ __forceinline__ void put_reply_words(const onc_msg& d, const EncSrc& 
 // RpcMessage::serialise_into (rpc_message.rs:136-164; MessageType :55-68)
 // up to the raw payload.
 // (cred_pre, when use_pre: the Call's AUTH_UNIX credential block, already loaded)
-// (dc: run the deferred checks of declared AUTH_UNIX auths, plan_record<true>)
+// (dc: run the deferred checks of a declared AUTH_UNIX credential, plan_record<true>)
 template <class Sink>
 __device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, Sink& out,
                                                  const UnixRegs* cred_pre = nullptr, bool use_pre = false,
@@ -455,7 +459,7 @@ __device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len,
     out(bswap(d.xid));
     out(bswap(uint32_t(d.msg_type)));
     if (d.msg_type == ONC_MSG_CALL) put_call_words(d, s, out, cred_pre, use_pre, dc);
-    else put_reply_words(d, s, out, dc);
+    else put_reply_words(d, s, out);
 }
 
 __device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len, const EncSrc& s, uint32_t* dst) {

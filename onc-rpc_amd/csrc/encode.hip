@@ -57,15 +57,22 @@ __global__ __launch_bounds__(kLenThreads) void enc_len_kernel(EncArgs a) {
             if (kRoot) {
                 p = plan_root(d[k], a.unix, a.bounds, a.root);
             } else {
-                // the plan of an emit takes declared AUTH_UNIX lengths as
+                // decl 1 (the plan of an emit): declared AUTH_UNIX lengths as
                 // given (no parameter-block load: the emit checks the block);
                 // a record failing that form is planned in full for its
-                // reference-order status (rare: only failing records)
+                // reference-order status (rare: only failing records).
+                // decl 2 (onc_encode_lengths): the same extent, every check
+                // up front for the status (include/onc_rpc.h onc_auth)
                 if (a.decl) p = plan_record<true>(d[k], a.unix, a.bounds);
-                if (!a.decl || p.status != ONC_OK) p = plan_record<false>(d[k], a.unix, a.bounds);
+                if (a.decl == 2) {
+                    const RecPlan f = plan_record<false>(d[k], a.unix, a.bounds);
+                    p.status = f.status;
+                } else if (!a.decl || p.status != ONC_OK) {
+                    p = plan_record<false>(d[k], a.unix, a.bounds);
+                }
             }
             len = p.len;
-            pay = len - 4ull * meta_hw(p.meta);           // 0 for a failing record (len = meta = 0)
+            pay = len - 4ull * meta_hw(p.meta);           // 0 for a record without extent (len = meta = 0)
             a.status[r] = p.status;
             if (a.rec_len) a.rec_len[r] = uint32_t(len);
             if (a.len_out) a.len_out[r] = uint32_t(len);
@@ -242,6 +249,7 @@ struct ImgTile {
     int4 ent[kEmitRecs + 1];         // {cf, NP + pure chunks, cp1, NP} (chunks, span-relative); [ns].x = sentinel
     uint4 pay[kEmitRecs + 1];        // {pst, en (bytes, span-chunk-relative; kNoPay both: no stream payload), src lo, hi}
     uint8_t map[kMap2Cap];           // granule -> span record owning its first chunk
+    int32_t bad[kEmitRecs];          // a declared credential's failing deferred check (0: none)
 };
 
 // Image slots are swizzled inside aligned groups of 8 (slot s lives at
@@ -552,6 +560,25 @@ __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, 
     }
 }
 
+// A tile whose declared AUTH_UNIX credentials failed their deferred checks
+// (T.bad; rare): once every store of the tile is done, each such record gets
+// its status and its header bytes zeroed in the output (the serialiser wrote
+// an empty parameter block in their place; the payload stays).
+__device__ __forceinline__ void declared_fixup(const EncArgs& a, const ImgTile& T, uint64_t r0, uint64_t T0) {
+    const int lane = threadIdx.x & 63;
+    __builtin_amdgcn_s_waitcnt(0);                    // the tile's stores (same wave) are done
+    if (r0 + lane >= a.n) return;
+    const int32_t st = T.bad[lane];
+    if (st == ONC_OK) return;
+    a.status[r0 + lane] = st;
+    const onc_msg d = a.msgs[r0 + lane];
+    const RecPlan p = plan_record<true>(d, a.unix, a.bounds);       // the extent it was placed with
+    const uint64_t start = a.origin + a.rec_off[r0 + lane];
+    const uint64_t end = min(uint64_t(start + 4ull * meta_hw(p.meta)), a.out_cap);
+    for (uint64_t b = start; b < end; ++b) a.out[b] = 0;
+    (void)T0;
+}
+
 template <int kU, int kNT, bool kFused, bool kRoot = false, bool kGiven = false, bool kPre = false,
           bool kLen = false>
 __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile, uint64_t given = 0) {
@@ -587,8 +614,11 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     uint64_t len = 0, poff = 0;
     uint32_t hw = 0;
     bool word_aligned = true;
-    // a Call's AUTH_UNIX credential: its parameter block is issued with the
-    // header build's descriptor reload (one round trip, not two dependent)
+    // kPre (lab, ONC_VARIANT_EMIT_PRELOAD): a Call's AUTH_UNIX credential
+    // block issued with the header build's descriptor reload (one round trip,
+    // not two dependent; round 3: c0 enc_emit 105 -> 102.5 us). With the
+    // declared-length checks it spills 4 VGPRs inside the gid writes (each
+    // reload a vmcnt(0) wait): c0 enc_emit 117 us against 98 without it.
     const bool cred_unix = kPre && !kRoot && dm.msg_type == ONC_MSG_CALL && (dm.cred.kind_len >> 24) == ONC_KIND_UNIX;
     const uint64_t cred_ref = dm.cred.ref;
     if (lane < nrec) {
@@ -637,6 +667,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
 
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.msgs);   // >= 64 valid bytes
     ONC_PROF(2);
+    if (!kRoot) T.bad[lane] = ONC_OK;
     int lo_rec = 0;
     while (lo_rec < nrec) {
         // span: records [lo_rec, hi_rec) whose non-pure chunks (+1 for a
@@ -656,7 +687,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         // records OR into the image: zero the slots this span uses (the
         // cut above bounds them by kImgChunks)
         // (whole groups of 8: the swizzle permutes inside a group)
-        const int used = int(min(uint64_t(kImgChunks), (lane_u64(wnp, hi_rec - 1) - wbase + 8) & ~7ull));
+        const int used = int(min(uint64_t(kImgChunks), uint64_t((lane_u64(wnp, hi_rec - 1) - wbase + 8) & ~7ull)));
         for (int k = lane; k < used; k += 64) T.img[k] = make_uint4(0, 0, 0, 0);
         const bool active = lane >= lo_rec && lane < hi_rec;
         const int j = lane - lo_rec;
@@ -690,25 +721,26 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                 const onc_msg d = as_msg(mr2);
                 const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
                 ImgSink w{img32, uint32_t(ibb >> 2), 32u - 8u * uint32_t(ibb & 3), 0u};
-                // declared AUTH_UNIX lengths: the parameter-block checks the
-                // plan deferred run on the block words the serialiser loads;
-                // a failing record keeps its extent with its header words
-                // cleared (include/onc_rpc.h onc_auth)
-                DeclCheck dc{a.bounds.auth_len, ONC_OK};
-                if (kRoot) {
-                    put_root_words(d, uint32_t(len), src, a.root, w);
-                } else {
-                    put_header_words(d, uint32_t(len), src, w, &cq, cred_unix, &dc);
-                    if (dc.st != ONC_OK) {
-                        a.status[r0 + lane] = dc.st;
-                        img_clear(img32, uint32_t(ibb), 4 * hw);
-                        w.prev = 0u;
-                    }
-                }
+                // a declared AUTH_UNIX credential: the parameter-block checks
+                // the plan deferred run on the block words the serialiser
+                // loads (or preloaded), which stops there; a failing record
+                // keeps its extent, the words written so far cleared
+                // (include/onc_rpc.h onc_auth). (Checking the preloaded block
+                // before the header build instead: 15 VGPRs spilled.)
+                // (the status lands in LDS and the record is fixed up when
+                // the tile is done: nothing extra live across the header
+                // build or the stream — 128 VGPRs without spills)
+                DeclCheck dc{a.bounds.auth_len, &T.bad[lane]};
+                if (kRoot) put_root_words(d, uint32_t(len), src, a.root, w);
+                else put_header_words(d, uint32_t(len), src, w, &cq, cred_unix, &dc);
                 if (small) {
                     // all of it lies in non-pure chunks (np = 0): right after
-                    // the header (bytes past its end read as zero)
+                    // the header (bytes past its end read as zero), by a sink
+                    // of its own (the header's last bytes flushed first: both
+                    // OR into the dword they share)
+                    w.finish();
                     const uintptr_t pb = sb + pst;
+                    w = ImgSink{img32, uint32_t(ibb >> 2) + hw, w.sh, 0u};
                     for (uint32_t k = 0; 4 * k < plen; ++k) w(load4_masked(pb + 4 * k, pb + plen));
                 } else if (kRoot && plen != 0 && pst < (uint64_t(cfa) << 4)) {
                     // a body root's header can be shorter than a chunk
@@ -744,6 +776,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         if (lo_rec == hi_rec && hi_rec == nrec) ONC_PROF(4);
     }
     ONC_PROF(5);
+    if (!kRoot && __any(lane < nrec && T.bad[lane] != ONC_OK)) declared_fixup(a, T, r0, T0);
 }
 
 // ---------------------------------------------------------------------------
@@ -881,7 +914,7 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
     const uint64_t S1 = lane_u64(Sen, hi_rec - 1);
     const int64_t C0 = int64_t(S0 >> 4);
     const uint64_t B0 = uint64_t(C0) << 4;
-    const int used = int(min(uint64_t(kImgChunks), (lane_u64(Swnp, hi_rec - 1) - wbase + 8) & ~7ull));
+    const int used = int(min(uint64_t(kImgChunks), uint64_t((lane_u64(Swnp, hi_rec - 1) - wbase + 8) & ~7ull)));
     for (int k = lane; k < used; k += 64) W.T.img[k] = make_uint4(0, 0, 0, 0);
     const bool active = lane >= lo_rec && lane < hi_rec;
     const int j = lane - lo_rec;
@@ -906,11 +939,13 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
             const onc_msg d = as_msg(mr2);
             const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
             ImgSink w{img32, uint32_t(ibb >> 2), 32u - 8u * uint32_t(ibb & 3), 0u};
-            DeclCheck dc{a.bounds.auth_len, ONC_OK};
+            int32_t bad = ONC_OK;
+            DeclCheck dc{a.bounds.auth_len, &bad};
             put_header_words(d, uint32_t(Slen), src, w, nullptr, false, &dc);
-            if (dc.st != ONC_OK) {                     // (see enc_emit_tile)
-                a.status[S.r0 + lane] = dc.st;
+            if (bad != ONC_OK) {                       // (see enc_emit_tile)
+                a.status[S.r0 + lane] = bad;
                 img_clear(img32, uint32_t(ibb), uint32_t(Spst - Sstart));
+                w.d = uint32_t(ibb >> 2) + uint32_t((Spst - Sstart) >> 2);
                 w.prev = 0u;
             }
             if (small) {
@@ -1053,8 +1088,7 @@ static_assert(kWsGrid / kTilesPerBlk <= 64, "a producer adds at most 64 workgrou
 // the grid's waves), placed by a running sum of the enc_len workgroup
 // totals, as the producer does.
 constexpr uint64_t kWsMinPayload = 128;     // bytes per record (the host rule's threshold)
-constexpr uint64_t kWsSample = 1024;        // enc_len workgroups summed (all of them up to 1M records — one
-                                            // chunk of a chunked encode — else every ceil(nb / 1024)-th)
+constexpr uint64_t kWsSample = 64;          // enc_len workgroups sampled, evenly spaced over the launch
 union WsShared {
     struct {
         WsSlot slot[2];
@@ -1063,28 +1097,19 @@ union WsShared {
     ImgTile wpt[4];
 };
 
-// The whole launch's payload, not its head (round 3 sampled the first 64
+// Sampled across the whole launch, not its head (round 3 read the first 64
 // workgroups, so a batch whose head and tail differ got the wrong kernel):
-// 16 loads per lane, issued together — the same one round trip.
+// 64 enc_len workgroups spaced evenly over the launch, one load per lane.
+// (Summing all 1024 of a 1M-record launch, 16 loads per lane in every
+// workgroup's prologue, cost configs[1]'s enc_emit 3.5 us.)
 __device__ __forceinline__ bool ws_header_heavy(const EncArgs& a) {
     if (!a.block_pay || (a.variant & ONC_VARIANT_WS_PIPELINE)) return false;   // the pipeline on every shape (tests)
     const int lane = threadIdx.x & 63;
     const uint64_t nb = num_len_blocks(a.n);
-    const uint64_t stride = (nb + kWsSample - 1) / kWsSample;
-    constexpr int kPer = int(kWsSample / 64);
-    uint64_t v[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        const uint64_t b = (uint64_t(lane) + 64ull * k) * stride;
-        v[k] = a.block_pay[b < nb ? b : nb - 1];
-    }
-    uint64_t pay = 0, recs = 0;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        const uint64_t b = (uint64_t(lane) + 64ull * k) * stride;
-        pay += b < nb ? v[k] : 0;
-        recs += b < nb ? min(uint64_t(kLenRecs), a.n - b * kLenRecs) : 0;
-    }
+    const uint64_t b = uint64_t(lane) * nb / kWsSample;       // strictly increasing while nb >= 64
+    const bool use = uint64_t(lane) < kWsSample && (nb >= kWsSample || uint64_t(lane) < nb);
+    const uint64_t pay = use ? a.block_pay[b] : 0;
+    const uint64_t recs = use ? min(uint64_t(kLenRecs), a.n - b * kLenRecs) : 0;
     return lane_u64(wave_incl_scan_u64(pay), 63) < kWsMinPayload * lane_u64(wave_incl_scan_u64(recs), 63);
 }
 
@@ -1106,7 +1131,7 @@ __device__ __forceinline__ void ws_as_wave_per_tile(const EncArgs& a, ImgTile& T
 }
 
 template <int kU, int kNT>
-__global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void enc_emit_ws_kernel(EncArgs a) {
     __shared__ WsShared s_sh;
     WsSlot* s_slot = s_sh.ws.slot;
     WsLane* s_ln = s_sh.ws.ln;
@@ -1189,16 +1214,15 @@ __global__ __launch_bounds__(256) void enc_emit_ws_kernel(EncArgs a) {
 // kNT: bit 0 = nontemporal payload loads, bit 1 = nontemporal stores (header
 // chunks stored temporally so that the decoder finds them cached made the
 // decode slower, 60 -> 69 us on c1: the dirty lines are written back at the
-// kernel boundary). The message instances are held to 4 waves per SIMD (128
-// VGPRs, no spills; the deferred AUTH_UNIX checks took them to 134, 3 waves);
-// squeezed to 5 waves per SIMD every shape measured slower (spills). The
-// body-root instances keep what they need (138 VGPRs).
-template <int kU, int kNT = 0, bool kFused = false, bool kRoot = false, bool kLen = false>
+// kernel boundary). The message instances need 106 VGPRs (4 waves per SIMD;
+// held there by the attribute); squeezed to 5 waves per SIMD (96 VGPRs) they
+// spill. The body-root instances keep what they need (140 VGPRs).
+template <int kU, int kNT = 0, bool kFused = false, bool kRoot = false, bool kLen = false, bool kPre = false>
 __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(kRoot ? 1 : 4))) void enc_emit_kernel_t(EncArgs a) {
     __shared__ ImgTile s_tiles[kFastWaves];
     const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
     if (tile < num_emit_tiles(a.n))
-        enc_emit_tile<kU, kNT, kFused, kRoot, false, !kRoot, kLen>(a, s_tiles[threadIdx.x >> 6], tile);
+        enc_emit_tile<kU, kNT, kFused, kRoot, false, kPre, kLen>(a, s_tiles[threadIdx.x >> 6], tile);
 }
 
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
@@ -1232,6 +1256,16 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     const dim3 g{uint32_t(blocks)}, b{uint32_t(64 * kFastWaves)};
+    if (a.variant & ONC_VARIANT_EMIT_PRELOAD) {     // (lab: the round-3 credential-block preload)
+        if (a.len_in) {
+            if (a.fused_base) ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, true, false, true, true>), g, b, 0, s, a);
+            else ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false, false, true, true>), g, b, 0, s, a);
+        } else {
+            if (a.fused_base) ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, true, false, false, true>), g, b, 0, s, a);
+            else ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false, false, false, true>), g, b, 0, s, a);
+        }
+        return hipGetLastError();
+    }
     if (a.len_in) {
         if (a.fused_base) ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, true, false, true>), g, b, 0, s, a);
         else ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false, false, true>), g, b, 0, s, a);

@@ -52,10 +52,15 @@ __global__ __launch_bounds__(kIovLenThreads) void iov_len_kernel(IovArgs a) {
         const uint64_t r = rw + 64 * k + lane;
         uint64_t len = 0, hl = 0;
         if (r < a.n) {
-            const RecPlan p = plan_record(as_msg(mr[k]), a.unix, a.bounds);
-            len = p.len;
-            hl = p.len ? 4ull * meta_hw(p.meta) : 0;
-            a.status[r] = p.status;
+            // the extent onc_encode gives the record (declared AUTH_UNIX
+            // lengths), the status of every check; header bytes only for an
+            // OK record (include/onc_rpc.h onc_auth)
+            const onc_msg d = as_msg(mr[k]);
+            const RecPlan p = plan_record<true>(d, a.unix, a.bounds);
+            const RecPlan f = plan_record<false>(d, a.unix, a.bounds);
+            len = p.status == ONC_OK ? p.len : 0;
+            hl = f.status == ONC_OK ? 4ull * meta_hw(f.meta) : 0;
+            a.status[r] = f.status;
         }
         // header bytes of 64 records < 2^15, so (len << 16 | hl) scans as one u64
         const uint64_t incl = wave_incl_scan_u64((len << 16) | hl);
@@ -131,8 +136,9 @@ __global__ __launch_bounds__(64 * kIovWaves) void iov_emit_kernel(IovArgs a) {
     uint64_t tsum = a.tile_sum[t0 + (uint64_t(lane) < kIovTilesPerBlk ? lane : 0)];
     const int nrec = live ? int(min(uint64_t(kEmitRecs), a.n - r0)) : 1;
     MsgRegs mr = issue_msg(a.msgs + (live ? r0 + min(lane, nrec - 1) : 0));
+    int32_t st0 = a.status[live ? r0 + min(lane, nrec - 1) : 0];      // iov_len's status
     asm volatile("" : "+v"(mr.q[0]), "+v"(mr.q[1]), "+v"(mr.q[2]), "+v"(mr.q[3]), "+v"(bl[0]), "+v"(bl[1]),
-                 "+v"(bl[2]), "+v"(bl[3]), "+v"(bh[0]), "+v"(bh[1]), "+v"(bh[2]), "+v"(bh[3]), "+v"(tsum));
+                 "+v"(bl[2]), "+v"(bl[3]), "+v"(bh[0]), "+v"(bh[1]), "+v"(bh[2]), "+v"(bh[3]), "+v"(tsum), "+v"(st0));
     if constexpr (kFused) {
         uint64_t vl = 0, vh = 0;
 #pragma unroll
@@ -171,10 +177,15 @@ __global__ __launch_bounds__(64 * kIovWaves) void iov_emit_kernel(IovArgs a) {
     uint32_t* hdr = s_hdr[wv];
     const onc_msg d = as_msg(mr);
     uint64_t len = 0, hl = 0;
+    bool rec_ok = false;
     if (lane < nrec) {
-        const RecPlan p = plan_record(d, a.unix, a.bounds);
-        len = p.len;
-        hl = p.len ? 4ull * meta_hw(p.meta) : 0;
+        // as iov_len: the extent from the declared lengths, header bytes for
+        // an OK record (iov_len's status: a record failing only a deferred
+        // block check keeps its extent, without header or iovec lengths)
+        const RecPlan p = plan_record<true>(d, a.unix, a.bounds);
+        len = p.status == ONC_OK ? p.len : 0;
+        rec_ok = len != 0 && st0 == ONC_OK;
+        hl = rec_ok ? 4ull * meta_hw(p.meta) : 0;
     }
     const uint64_t sv = (len << 16) | hl;
     const uint64_t incl = wave_incl_scan_u64(sv);
@@ -185,8 +196,8 @@ __global__ __launch_bounds__(64 * kIovWaves) void iov_emit_kernel(IovArgs a) {
     const uint64_t Ht = last & 0xFFFFu;                  // header bytes of the tile
     const bool fits = hoff + hl <= a.hdr_cap;
     if (lane < nrec) {
-        const bool ok = len != 0 && fits;
-        if (len != 0 && !fits) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
+        const bool ok = rec_ok && fits;
+        if (rec_ok && !fits) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
         u32x4* e = reinterpret_cast<u32x4*>(a.iov + r0 + lane);
         const uint64_t po = ok ? d.payload_off : 0;
         const uint32_t pl = ok ? uint32_t(len - hl) : 0u;

@@ -57,8 +57,9 @@ struct EncArgs {
     uint32_t variant;       // ONC_VARIANT_* bits (onc_codec_options; A/B experiments, tests)
     uint32_t ws;            // enc_emit: the wave-specialised kernel (codec.hip enc_args decides)
     uint32_t root;          // ONC_ROOT_* (onc_encode_body); ONC_ROOT_RPC_MESSAGE for onc_encode
-    uint32_t decl;          // enc_len of an emit's plan: declared AUTH_UNIX lengths taken as given (the
-                            // emit runs the deferred parameter-block checks); 0: every check (onc_encode_lengths)
+    uint32_t decl;          // enc_len, RpcMessage root: 1 = an emit's plan (declared AUTH_UNIX lengths taken
+                            // as given, the emit runs the deferred parameter-block checks); 2 = onc_encode_lengths
+                            // (the same extents, every check up front for the statuses); 0 = every check (roots)
     const uint64_t* base_dev;   // optional: output bytes before this launch's first record (chunked encode)
     const uint32_t* len_in;     // optional (wave-per-tile enc_emit): the plan's record lengths, read instead
                                 // of re-planning (no dependent AUTH_UNIX parameter load in the prologue)
@@ -74,6 +75,8 @@ constexpr uint64_t kFusedBlocks = 1024;
 
 struct IovArgs {
     uint64_t n;
+    // (extents follow the declared AUTH_UNIX lengths as onc_encode places them; a record failing only a
+    // deferred block check takes its extent with no header bytes and a zero-length iovec)
     const onc_msg* msgs;
     const onc_unix_params* unix;
     const uint8_t* auth_arena;

@@ -933,8 +933,9 @@ int32_t oracle_encode_message(const onc_msg* msg, const onc_unix_params* unix_ta
  * So a record that fails only a block check (a panic of AuthUnixParams::new /
  * Gids, or declared != serialised length) still takes the extent the
  * descriptor declares: its header bytes zero, its payload (a Call's, an
- * accepted Success's) in place. Returns 1 with that extent and header size
- * when every descriptor-only check passes (encode.hip plan_record<true>). */
+ * accepted Success's) in place. Only a Call's credential is planned that way
+ * (a verifier's block is checked up front). Returns 1 with that extent and
+ * header size when every other check passes (encode.hip plan_record<true>). */
 static int declared_extent(const onc_msg* d, const onc_unix_params* unix_table, uint64_t* len, uint64_t* hdr) {
     /* one auth: serialised_len (id + body) and associated_data_len bound */
     uint64_t aw[2] = {0, 0}, assoc[2] = {0, 0};
@@ -947,13 +948,14 @@ static int declared_extent(const onc_msg* d, const onc_unix_params* unix_table, 
         const onc_auth* a = auths[k];
         const uint32_t kind = ONC_AUTH_KIND(*a), l = ONC_AUTH_LEN(*a);
         if (kind > ONC_KIND_UNKNOWN) return 0;
-        if (kind == ONC_KIND_UNIX && l != 0) {
+        if (kind == ONC_KIND_UNIX && l != 0 && k == 0) {      /* only a Call's credential is deferred */
             if (l < 20 || (l & 3) || l > 20 + 4 * 64 + 4 * 16) return 0;   /* implausible */
             aw[k] = 8 + l;
             assoc[k] = l - 8;                         /* > 200 exactly when the true value is */
         } else if (kind == ONC_KIND_UNIX) {
             const onc_unix_params* p = &unix_table[a->ref];
             if (p->name_len > ONC_MAX_MACHINE_NAME_LEN || p->ngids > ONC_MAX_GIDS) return 0;
+            if (l != 0 && l != 20 + 4 * ((p->name_len + 3) / 4) + 4 * p->ngids) return 0;   /* declared != serialised */
             aw[k] = 8 + 20 + 4 * ((p->name_len + 3) / 4) + 4ull * p->ngids;
             assoc[k] = 12 + p->name_len + 4ull * p->ngids;
         } else {

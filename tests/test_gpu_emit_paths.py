@@ -19,8 +19,9 @@ pytestmark = pytest.mark.gpu
 # ws: the wave-specialised kernel, which runs header-heavy batches as
 # wave-per-tile workers (encode.hip ws_header_heavy); ws_pipeline: the same
 # kernel with that fallback off (0x10000), its producer/consumer pipeline
-# on every shape; tile: the wave-per-tile kernel
-PATHS = {"ws": 0x200, "ws_pipeline": 0x10200, "tile": 0x400}
+# on every shape; tile: the wave-per-tile kernel; tile_preload: the same with
+# the AUTH_UNIX credential block preloaded (0x80000, lab)
+PATHS = {"ws": 0x200, "ws_pipeline": 0x10200, "tile": 0x400, "tile_preload": 0x80400}
 
 
 @pytest.fixture(scope="module")
@@ -218,7 +219,8 @@ def test_declared_lengths_broken_blocks(codec, R, oracle, seed):
     check's status; the others get the full plan's reference-order status
     and no bytes — the oracle's restatement of the rule, bit-exact, at two
     writer positions and with a capacity inside the batch. onc_encode_lengths
-    checks every block up front (failing records: length 0)."""
+    checks every block up front and reports the same extents (what a caller
+    sizes its send buffer with)."""
     import torch
     hb = _adversarial(seed)
     o_st, o_len = _enc_oracle_sized(R, codec, hb, oracle)
@@ -232,7 +234,7 @@ def test_declared_lengths_broken_blocks(codec, R, oracle, seed):
     codec.encode_lengths(db, rl, st)
     codec.sync()
     assert np.array_equal(st.cpu().numpy(), o_st)
-    assert np.array_equal(rl.cpu().numpy().view(np.uint32), np.where(o_st == 0, o_len, 0))
+    assert np.array_equal(rl.cpu().numpy().view(np.uint32), o_len)
 
 
 def test_declared_equals_undeclared(codec, R, oracle):

@@ -102,6 +102,9 @@ def test_descriptor_bounds(codec, R, oracle):
     cu = np.nonzero(is_call & ((m["cred_kind_len"] >> 24) == L.KIND_UNIX) & ~bad)[0]
     idx = rng.choice(cu, 30, replace=False)
     m["cred_ref"][idx] = np.uint64(n_unix)
+    # (undeclared: index n_unix is the private row below, whose name lies
+    # outside the arena — a declared credential keeps its extent then)
+    m["cred_kind_len"][idx] = int(L.pack_kind_len(L.KIND_UNIX, 0))
     bad[idx] = True
     # opaque auth body past the arena
     op = np.nonzero(is_call & ((m["verf_kind_len"] >> 24) != L.KIND_UNIX) & ((m["verf_kind_len"] & 0xFFFFFF) > 0)
@@ -115,6 +118,9 @@ def test_descriptor_bounds(codec, R, oracle):
     unix2["name_off"][-1] = auth_len - 2
     cu = np.nonzero(is_call & ((m["cred_kind_len"] >> 24) == L.KIND_UNIX) & ~bad)[0][:10]
     m["cred_ref"][cu] = len(unix2) - 1
+    # (undeclared: a declared credential's name is checked by the emit and the
+    # record keeps its extent — test_gpu_emit_paths.py::test_declared_name_outside_arena)
+    m["cred_kind_len"][cu] = int(L.pack_kind_len(L.KIND_UNIX, 0))
     bad[cu] = True
     # device batch: physical tensors padded well past the declared sizes
     pad = 4096
