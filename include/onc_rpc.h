@@ -355,6 +355,8 @@ typedef struct onc_codec onc_codec;
 #define ONC_VARIANT_EMIT_REPLAN      0x20000u  /* wave-per-tile enc_emit re-plans instead of reading the plan's lengths */
 #define ONC_VARIANT_WHOLE_PLAN       0x40000u  /* plan a large batch whole instead of in chunks */
 #define ONC_VARIANT_EMIT_PRELOAD     0x80000u  /* wave-per-tile enc_emit: preload the AUTH_UNIX credential block (lab) */
+#define ONC_VARIANT_DEC_AUX_SPARSE   0x100000u /* decode: aux0/aux1 written only for failing records (lab;
+                                                  the outputs of OK records' aux words are then undefined) */
 
 #define ONC_OPT_FORCE_SCAN 0x1u   /* always launch the separate block-scan kernels (tests of that path) */
 

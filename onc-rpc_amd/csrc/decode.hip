@@ -742,8 +742,12 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
         if (kRoot && a.consumed) a.consumed[i] = st == ONC_OK ? consumed : 0u;
         if (kNTOut) {
             __builtin_nontemporal_store(st, a.out.status + i);
-            __builtin_nontemporal_store(aux0, a.out.aux0 + i);
-            __builtin_nontemporal_store(aux1, a.out.aux1 + i);
+            // (lab, ONC_VARIANT_DEC_AUX_SPARSE: aux words only for failing
+            // records — 8 of the 76 bytes written per OK record)
+            if (!(a.variant & ONC_VARIANT_DEC_AUX_SPARSE) || st != ONC_OK) {
+                __builtin_nontemporal_store(aux0, a.out.aux0 + i);
+                __builtin_nontemporal_store(aux1, a.out.aux1 + i);
+            }
         } else {
             a.out.status[i] = st;
             a.out.aux0[i] = aux0;

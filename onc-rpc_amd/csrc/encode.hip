@@ -1081,13 +1081,13 @@ static_assert(kWsGrid / kTilesPerBlk <= 64, "a producer adds at most 64 workgrou
 // Header-heavy batches (codec.hip picks this kernel from the declared payload
 // arena, which overstates the payload when it is a decoded wire: a re-encode
 // of configs[0]-shaped records measured enc_emit 99 -> 159 us): every
-// workgroup samples the enc_len totals of the first kWsSample workgroups
-// (enc_len's block_pay: streamed payload bytes) and, when the records
-// average under kWsMinPayload payload bytes, its four waves run the
-// wave-per-tile code instead — each wave its own tiles (g, g + G, ...; G =
-// the grid's waves), placed by a running sum of the enc_len workgroup
-// totals, as the producer does.
-constexpr uint64_t kWsMinPayload = 128;     // bytes per record (the host rule's threshold)
+// workgroup samples the enc_len totals of kWsSample workgroups spread over
+// the launch (enc_len's block_pay: streamed payload bytes; block_sum: all
+// bytes) and, when the payload is under kWsPayPerHeader times the header
+// bytes, its four waves run the wave-per-tile code instead — each wave its
+// own tiles (g, g + G, ...; G = the grid's waves), placed by a running sum of
+// the enc_len workgroup totals, as the producer does.
+constexpr uint64_t kWsPayPerHeader = 4;     // the pipeline when payload >= 4 x header bytes
 constexpr uint64_t kWsSample = 64;          // enc_len workgroups sampled, evenly spaced over the launch
 union WsShared {
     struct {
@@ -1097,11 +1097,19 @@ union WsShared {
     ImgTile wpt[4];
 };
 
-// Sampled across the whole launch, not its head (round 3 read the first 64
-// workgroups, so a batch whose head and tail differ got the wrong kernel):
-// 64 enc_len workgroups spaced evenly over the launch, one load per lane.
-// (Summing all 1024 of a 1M-record launch, 16 loads per lane in every
-// workgroup's prologue, cost configs[1]'s enc_emit 3.5 us.)
+// The rule (round 4, tools/mix_lab.py sweep, profiles/lab_r04_mix_sweep.log):
+// the pipeline's single producer stages header bytes while three consumers
+// stream payload, so the pipeline wins once the payload is about four times
+// the header bytes — AUTH_NONE calls (44-byte headers): 128 B payloads 61 us
+// wave-per-tile against 67 pipelined, 192 B 93 / 92, 256 B 119 / 106;
+// AUTH_UNIX 16-gid calls (128 B): 256 B 152 / 178, 512 B 250 / 245; a quarter
+// of configs[0]'s records among configs[1]'s (3.2x) 117 / 122. (Round 3's
+// rule, payload >= 128 B per record, sent a half/half mix of the two to the
+// pipeline: 130 us against 107.) Sampled across the whole launch, not its
+// head (round 3 read the first 64 workgroups only): 64 enc_len workgroups
+// spaced evenly, their byte and payload totals, one load of each per lane.
+// (Summing all 1024 workgroups of a 1M-record launch in every workgroup's
+// prologue cost configs[1]'s enc_emit 3.5 us.)
 __device__ __forceinline__ bool ws_header_heavy(const EncArgs& a) {
     if (!a.block_pay || (a.variant & ONC_VARIANT_WS_PIPELINE)) return false;   // the pipeline on every shape (tests)
     const int lane = threadIdx.x & 63;
@@ -1109,8 +1117,9 @@ __device__ __forceinline__ bool ws_header_heavy(const EncArgs& a) {
     const uint64_t b = uint64_t(lane) * nb / kWsSample;       // strictly increasing while nb >= 64
     const bool use = uint64_t(lane) < kWsSample && (nb >= kWsSample || uint64_t(lane) < nb);
     const uint64_t pay = use ? a.block_pay[b] : 0;
-    const uint64_t recs = use ? min(uint64_t(kLenRecs), a.n - b * kLenRecs) : 0;
-    return lane_u64(wave_incl_scan_u64(pay), 63) < kWsMinPayload * lane_u64(wave_incl_scan_u64(recs), 63);
+    const uint64_t all = use ? a.block_sum[b] : 0;
+    const uint64_t p = lane_u64(wave_incl_scan_u64(pay), 63), t = lane_u64(wave_incl_scan_u64(all), 63);
+    return p < kWsPayPerHeader * (t - p);
 }
 
 template <int kU, int kNT>

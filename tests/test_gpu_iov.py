@@ -124,3 +124,31 @@ def test_iov_maximal_headers(codec, R, oracle):
                      "cred": cred, "verf": verf, "payload": rng.bytes(int(rng.integers(0, 40))).hex()})
     hb = L.build_batch(msgs)
     check(hb, oracle, *gpu_iov(R, codec, hb))
+
+
+def test_iov_declared_extents(codec, R, oracle):
+    """Declared AUTH_UNIX credentials whose blocks fail the deferred checks
+    (tests/test_gpu_emit_paths.py::_adversarial): the vectored encode places
+    records as onc_encode does (wire_off = the oracle's offsets for every
+    record, a failing record's declared extent included; totals[1] = the
+    packed total), the statuses are the oracle's, a failing record has zero
+    header and payload lengths, and every OK record's header bytes and
+    payload slice are the oracle's."""
+    from test_gpu_emit_paths import _adversarial
+    hb = _adversarial(75, n=2500)
+    o_wire, o_off, o_st, o_len = oracle.encode_batch(hb)
+    assert ((o_st != 0) & (o_len != 0)).any()
+    hdr, iov, st, tot = gpu_iov(R, codec, hb)
+    assert np.array_equal(st, o_st)
+    assert np.array_equal(iov["wire_off"], o_off[:-1])
+    assert int(tot[1]) == int(o_off[-1])
+    ok = st == 0
+    assert (iov["hdr_len"][~ok] == 0).all() and (iov["payload_len"][~ok] == 0).all()
+    w = np.frombuffer(o_wire, np.uint8)
+    for i in np.nonzero(ok)[0]:
+        e = iov[i]
+        a, hl, pl = int(o_off[i]), int(e["hdr_len"]), int(e["payload_len"])
+        assert hl + pl == int(o_len[i])
+        assert hdr[int(e["hdr_off"]):int(e["hdr_off"]) + hl].tobytes() == w[a:a + hl].tobytes()
+        po = int(e["payload_off"])
+        assert hb.payload_arena[po:po + pl].tobytes() == w[a + hl:a + hl + pl].tobytes()

@@ -66,6 +66,7 @@ def _caps(hbs, oracle):
 
 @pytest.mark.parametrize("kind,n,opts,lengths", [
     ("call_none", 20_000, {}, False),
+    ("call_none", 1_100_000, {}, True),                  # above one 1M-record plan chunk
     ("mixed", 9_001, {"enc_chunk": 2048}, True),          # the chunked encode: chunk k+1 reads k's end
     ("unix16", 5_000, {"enc_chunk": 2048, "variant": 0x400}, True),   # the emit reads the plan's lengths
     ("mixed", 6_000, {"decode_policy": 2}, False),
@@ -77,7 +78,7 @@ def test_graph_capture_replay_new_inputs(R, oracle, kind, n, opts, lengths):
     replay bit-exact vs the oracle (wire bytes, offsets, statuses, decoded
     descriptors, AUTH_UNIX slots, aux words)."""
     import torch
-    hbs = _batches(kind, n, [11, 12, 13, 14, 15])
+    hbs = _batches(kind, n, [11, 12, 13] if n > 100_000 else [11, 12, 13, 14, 15])
     slots = _Slots(R, n, *_caps(hbs, oracle))
     s = torch.cuda.Stream()
     codec = R.Codec(0, stream=s.cuda_stream, **opts)
