@@ -1,9 +1,11 @@
 """Lab: how cold is "cold"? configs[2]'s decode (onc_decode_lengths of 1M
 mixed records) timed with the codec's HIP events while rotating over K
 identical wire copies (K = 1 is the warm case; bench.py --cache cold uses
-K = 5), and with an untimed 1 GiB scrub (a torch fill of another buffer)
-before every decode of one copy. If the K >= 3 times and the scrub time
-agree, the rotation reaches the cold steady state.
+K = 5), and with an untimed 1 GiB scrub of another buffer before every
+decode of one copy: a write scrub (torch fill: leaves L2 + Infinity Cache
+full of dirty lines, written back while the decode reads) and a read scrub
+(torch sum: evicts without dirtying). If the K >= 3 times and the read-scrub
+time agree, the rotation reaches the clean cold steady state.
 
 Usage (GPU box): python tools/cold_lab.py [records] [reps]
 """
@@ -40,15 +42,19 @@ def main():
     c.sync()
     dec = R.DecodeBuffers(n)
     copies = [wire] + [wire.clone() for _ in range(8)]
-    scrub = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    scrub = torch.ones(1 << 30, dtype=torch.uint8, device="cuda")
+    scrub_words = scrub.view(torch.int32)
+    sink = torch.zeros(2, dtype=torch.int64, device="cuda")
 
-    def run(k, do_scrub=False):
+    def run(k, do_scrub=None):
         c.sync()
         c.reset_stats()
         c.enable_timing(True, kernels=[R.K_DEC_PARSE])
         for i in range(reps + 2):
-            if do_scrub:
+            if do_scrub == "write":
                 scrub.fill_(i & 0xFF)
+            elif do_scrub == "read":
+                sink[i % 2] = scrub_words.sum()
             c.decode_lengths(copies[i % k], rl, n, 0, L.DECODE_SLICE, dec.msgs, dec.unix, dec.status, dec.aux0,
                              dec.aux1)
         ms, cnt = c.kernel_stats()["decode_kernel"]
@@ -58,8 +64,9 @@ def main():
 
     for k in (1, 2, 3, 5, 9):
         print(f"copies {k}: decode {run(k):.1f} us", flush=True)
-    print(f"1 GiB scrub before each decode of one copy: decode {run(1, True):.1f} us", flush=True)
-    print(f"1 GiB scrub + 5 copies: decode {run(5, True):.1f} us", flush=True)
+    for kind in ("write", "read"):
+        print(f"1 GiB {kind} scrub before each decode of one copy: decode {run(1, kind):.1f} us", flush=True)
+        print(f"1 GiB {kind} scrub + 5 copies: decode {run(5, kind):.1f} us", flush=True)
 
 
 if __name__ == "__main__":

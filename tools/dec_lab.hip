@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <string>
 #include <vector>
 
 #include "../onc-rpc_amd/csrc/decode.hip"
@@ -135,6 +136,17 @@ __global__ __launch_bounds__(256) void l_write(DecArgs a) {
     }
 }
 
+// read scrub: every 16 bytes of the buffer folded into one word (evicts
+// L2 / MALL without leaving dirty lines behind, unlike a memset)
+__global__ __launch_bounds__(256) void scrub_read(const u32x4* p, uint64_t n16, uint32_t* sink) {
+    uint32_t x = 0;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * 256) {
+        const u32x4 v = p[i];
+        x ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (x == 0x9e3779b9u) sink[0] = x;
+}
+
 static void put32(uint8_t* p, uint32_t v) {
     p[0] = v >> 24; p[1] = v >> 16; p[2] = v >> 8; p[3] = v;
 }
@@ -187,9 +199,18 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const bool cold = getenv("LAB_WARM") == nullptr;
+    // LAB_SCRUB=read: a read sweep instead of the memset (the memset leaves up
+    // to L2 + MALL of dirty lines, written back while the timed kernel reads)
+    const bool rscrub = getenv("LAB_SCRUB") && std::string(getenv("LAB_SCRUB")) == "read";
+    uint32_t* sink;
+    CK(hipMalloc(&sink, 4));
+    CK(hipMemset(scrub, 7, scrub_b));
     for (int rep = 0; rep < 25; ++rep) {
         for (auto& v : vs) {
-            if (cold) CK(hipMemsetAsync(scrub, rep, scrub_b, 0));
+            if (cold && rscrub)
+                hipLaunchKernelGGL(scrub_read, dim3(8192), dim3(256), 0, 0, (const u32x4*)scrub, scrub_b / 16, sink);
+            else if (cold)
+                CK(hipMemsetAsync(scrub, rep, scrub_b, 0));
             CK(hipEventRecord(e0, 0));
             v.run();
             CK(hipEventRecord(e1, 0));
@@ -198,7 +219,7 @@ int main(int argc, char** argv) {
             if (rep >= 5) v.t.push_back(ms * 1000.f);
         }
     }
-    printf("n=%llu W=%u cold=%d\n", (unsigned long long)n, W, int(cold));
+    printf("n=%llu W=%u cold=%d scrub=%s\n", (unsigned long long)n, W, int(cold), rscrub ? "read" : "memset");
     for (auto& v : vs) {
         std::sort(v.t.begin(), v.t.end());
         printf("%-26s median %7.1f us  min %7.1f\n", v.name, v.t[v.t.size() / 2], v.t[0]);
