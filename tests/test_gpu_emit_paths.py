@@ -131,6 +131,28 @@ def test_two_span_edges(codec, R, oracle, shift):
     _check(R, codec, oracle, hb, shift=shift, cap=cap)
 
 
+@pytest.mark.parametrize("ntiles,last", [(1025, 5), (1024 + 300, 64), (1024 + 511, 33), (1024 + 600, 64),
+                                         (2048 + 3, 1)])
+def test_last_round_split(codec, R, oracle, ntiles, last):
+    """Tile counts around multiples of the wave-specialised kernel's 1024
+    persistent workgroups (a last round of 1, 300, 511 and 600 tiles, and
+    of 3 after two full rounds), a last tile of 5 records and one of a
+    single record: configs[1]-shaped records at writer positions 0 and 7
+    (the word and the byte path), a mixed batch with invalid records, and a
+    capacity ending inside the last round. (Round 4 measured cutting the
+    last round's tiles into parts, one per workgroup, and did not keep it:
+    the shapes stay as its tests.)"""
+    n = 64 * (ntiles - 1) + last
+    hb = S.call_none(n, 256, seed=ntiles)
+    _check(R, codec, oracle, hb)
+    _check(R, codec, oracle, hb, shift=7)
+    mx = S.mixed(n, seed=ntiles + 1, pmin=100, pmax=700, exotic=0.1)
+    _check(R, codec, oracle, mx, shift=3)
+    o_off = oracle.encode_batch(mx)[1]
+    cap = int(o_off[64 * (ntiles - 2) + 20]) + 5
+    _check(R, codec, oracle, mx, shift=3, cap=cap)
+
+
 def test_maximal_auth_unix(codec, R, oracle):
     """Credential and verifier both AUTH_UNIX at the 200-byte limit (460-byte
     headers) with odd payloads: several spans per tile on the byte path."""

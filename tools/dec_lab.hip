@@ -183,7 +183,7 @@ int main(int argc, char** argv) {
     const uint32_t grid = uint32_t((n + 255) / 256);
     struct V { const char* name; std::function<void()> run; std::vector<float> t; };
     std::vector<V> vs = {
-        {"product decode<slice>", [&] { hipLaunchKernelGGL(decode_kernel<ONC_DECODE_SLICE>, dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"product decode<slice>", [&] { hipLaunchKernelGGL(decode_kernel<ONC_DECODE_SLICE>, dim3(uint32_t((n + kDecTile - 1) / kDecTile)), dim3(kDecTile), 0, 0, a); }, {}},
         {"read 4 chunks", [&] { hipLaunchKernelGGL(l_read<4>, dim3(grid), dim3(256), 0, 0, a); }, {}},
         {"read 3 chunks", [&] { hipLaunchKernelGGL(l_read<3>, dim3(grid), dim3(256), 0, 0, a); }, {}},
         {"read 4 + write", [&] { hipLaunchKernelGGL(l_rw<4>, dim3(grid), dim3(256), 0, 0, a); }, {}},
