@@ -845,7 +845,15 @@ __device__ __forceinline__ WsLoads ws_issue(const EncArgs& a, uint64_t run_blk, 
     return L;
 }
 
-__device__ __forceinline__ void ws_begin_tile(const EncArgs& a, WsTile& S, WsLane* ln, uint64_t tile, WsLoads pf) {
+// The tile's descriptors as the prologue loaded them, kept in LDS for the
+// header builds of its spans ([quarter][lane]: conflict-free b128 accesses)
+// instead of a second load from L2 per span (a dependent round trip on the
+// producer's path while the consumers hold the memory system busy).
+struct WsDesc {
+    u32x4 q[4][64];
+};
+__device__ __forceinline__ void ws_begin_tile(const EncArgs& a, WsTile& S, WsLane* ln, WsDesc& dsc, uint64_t tile,
+                                              WsLoads pf) {
     const int lane = threadIdx.x & 63;
     const uintptr_t payload = reinterpret_cast<uintptr_t>(a.payload_arena);
     S.tile = tile;
@@ -856,6 +864,8 @@ __device__ __forceinline__ void ws_begin_tile(const EncArgs& a, WsTile& S, WsLan
     const uint64_t t0 = blk * kTilesPerBlk;
     const uint64_t tv = pf.tv, bw = pf.bw;
     const MsgRegs mr = pf.mr;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dsc.q[k][lane] = mr.q[k];
     S.run_base += lane_u64(wave_incl_scan_u64(S.run_blk + lane < blk ? bw : 0), 63);
     S.run_blk = blk;
     const uint64_t T0 = a.origin + S.run_base + lane_u64(wave_incl_scan_u64(t0 + lane < tile ? tv : 0), 63);
@@ -895,7 +905,8 @@ __device__ __forceinline__ void ws_begin_tile(const EncArgs& a, WsTile& S, WsLan
 
 // The next span of the producer's tile into slot W (image, entries, map,
 // header); advances S.lo_rec.
-__device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const WsLane* ln, WsSlot& W) {
+__device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const WsLane* ln, const WsDesc& dsc,
+                                              WsSlot& W) {
     const int lane = threadIdx.x & 63;
     const WsLane L = ln[lane];
     const uint64_t Slen = L.len, Spoff = L.poff, Sstart = L.start, Sen = L.en, Spst = L.pst, Swnp = L.wnp;
@@ -934,8 +945,9 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
         W.T.pay[j] = make_uint4(nopay ? kNoPay : ps, nopay ? kNoPay : pe, uint32_t(sb), uint32_t(sb >> 32));
         if (Slen != 0) {
             const uint64_t ibb = Sstart - 16ull * uint64_t(C0 + NP);
-            MsgRegs mr2 = issue_msg(a.msgs + S.r0 + lane);
-            asm volatile("" : "+v"(mr2.q[0]), "+v"(mr2.q[1]), "+v"(mr2.q[2]), "+v"(mr2.q[3]));
+            MsgRegs mr2;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) mr2.q[k] = dsc.q[k][lane];
             const onc_msg d = as_msg(mr2);
             const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
             ImgSink w{img32, uint32_t(ibb >> 2), 32u - 8u * uint32_t(ibb & 3), 0u};
@@ -1093,6 +1105,7 @@ union WsShared {
     struct {
         WsSlot slot[2];
         WsLane ln[64];
+        WsDesc desc;
     } ws;
     ImgTile wpt[4];
 };
@@ -1144,6 +1157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     __shared__ WsShared s_sh;
     WsSlot* s_slot = s_sh.ws.slot;
     WsLane* s_ln = s_sh.ws.ln;
+    WsDesc& s_desc = s_sh.ws.desc;
     const int wv = threadIdx.x >> 6;
     if (ws_header_heavy(a)) {                       // wave-uniform and grid-uniform
         ws_as_wave_per_tile<1, kNT>(a, s_sh.wpt[wv]);
@@ -1162,7 +1176,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
             WsLoads pf = ws_issue(a, S.run_blk, next);
             asm volatile("" : "+v"(pf.mr.q[0]), "+v"(pf.mr.q[1]), "+v"(pf.mr.q[2]), "+v"(pf.mr.q[3]), "+v"(pf.tv),
                          "+v"(pf.bw));
-            ws_begin_tile(a, S, s_ln, next, pf);
+            ws_begin_tile(a, S, s_ln, s_desc, next, pf);
             next += gridDim.x;
             have = true;
         }
@@ -1170,7 +1184,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
             if ((threadIdx.x & 63) == 0) W.h.state = 2u;
             return;
         }
-        ws_stage_span(a, S, s_ln, W);
+        ws_stage_span(a, S, s_ln, s_desc, W);
         if (S.lo_rec >= S.nrec) have = false;
     };
 #ifdef ONC_EMIT_PROF
