@@ -228,7 +228,7 @@ constexpr int kMap2Cap = ONC_MAP_CAP;         // granules per span (granule = 4 
 #define ONC_EMIT_U 1
 #endif
 constexpr int kEmitChunkUnroll = ONC_EMIT_U;    // chunks per lane per pipelined step
-constexpr int kEmitNT = 2;                    // nontemporal output stores (loads: measured slower)
+constexpr int kEmitNT = 2;                    // nontemporal output stores (loads: only for long payloads, launch_enc_emit)
 constexpr uint64_t kSpanBytesMax = 1ull << 30;  // a span's offsets fit uint32 (one record may exceed it)
 // A record's own non-pure chunks: its header is at most 4 * (7 + 2 * 54)
 // = 460 bytes (a Call whose cred and verifier are both AUTH_UNIX at the
@@ -1262,7 +1262,11 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
         // (a grid trimmed to equal tiles per workgroup, 977 for configs[1],
         // measured slower: concurrency beats the ragged last phase)
         const uint32_t g = uint32_t(min(uint64_t(kWsGrid), tiles));
-        if (a.ws == 2) ONC_LAUNCH((enc_emit_ws_kernel<1, kEmitNT>), dim3(g), dim3(256), 0, s, a);
+        // long payloads (>= 512 B on average, configs[3]) also load them
+        // nontemporally: the stream does not evict the descriptors and
+        // parameter blocks the producer reads (configs[3] enc_emit 442 ->
+        // 423 us per 1M chunk; configs[1]-shaped batches measured no gain)
+        if (a.ws == 2) ONC_LAUNCH((enc_emit_ws_kernel<1, kEmitNT | 1>), dim3(g), dim3(256), 0, s, a);
         else ONC_LAUNCH((enc_emit_ws_kernel<ONC_WS_U, kEmitNT>), dim3(g), dim3(256), 0, s, a);
         return hipGetLastError();
     }
