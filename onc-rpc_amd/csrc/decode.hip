@@ -527,9 +527,13 @@ __device__ __forceinline__ uint32_t stage_window(uint32_t* s_win, int t, uintptr
                                                  uint32_t d0, uint64_t L, bool& needs2) {
     const uint32_t avail = uint32_t(min(uint64_t(kWinChunks), (q0 + L + 15) >> 4));
     const uint32_t r44 = kPolicy ? uint32_t(min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4)) : kWin1;
-    // line policy: also the rest of the record's first 128-byte line
+    // line policy: also the rest of the record's first 128-byte line, and
+    // at least the record's first 128 bytes (a record starting inside a line
+    // takes the next line in round 1 too: configs[0]'s 128-byte headers 192
+    // bytes apart, half of them across a line boundary)
     const uint32_t rln = uint32_t((((win | 127u) + 1u) - win) >> 4);
-    const uint32_t r1 = kLine ? min(kWin1L, max(r44, rln)) : r44;
+    const uint32_t r128 = uint32_t((q0 + min(L, uint64_t(128)) + 15) >> 4);
+    const uint32_t r1 = kLine ? min(kWin1L, max(max(r44, rln), r128)) : r44;
     uint32_t nch = min(r1, avail);
     // all round-1 loads issued without a per-chunk branch (chunks past
     // the record's last granule re-read that granule) and pinned: under
