@@ -178,3 +178,53 @@ def test_codec_options_validated(R):
         c.set_decode_policy(R.DECODE_POLICY_LINE)
     finally:
         c.close()
+
+
+def test_two_codecs_on_two_streams_concurrently(R, oracle):
+    """Two codecs, each on its own stream, encode and decode different
+    batches with their work interleaved on the device: a configs[1]-shaped
+    batch (the wave-specialised kernel, a persistent grid of 1024
+    workgroups — two such grids cannot both be resident, and neither waits
+    on the other's workgroups) and a configs[0]-shaped one (the
+    wave-per-tile kernel). Each codec's scratch and decode policy are its
+    own (include/onc_rpc.h: one handle per stream); every output bit-exact
+    vs the oracle."""
+    import torch
+    batches = [S.call_none(150_000, 256, seed=71), S.cpu_roundtrip(60_000, seed=72)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    codecs = [R.Codec(0, stream=s.cuda_stream) for s in streams]
+    try:
+        bufs = []
+        for hb, c in zip(batches, codecs):
+            db = R.DeviceBatch.from_host(hb)
+            o_wire = oracle.encode_batch(hb)[0]
+            out = torch.zeros(len(o_wire) + 64, dtype=torch.uint8, device="cuda")
+            off = torch.zeros(hb.n + 1, dtype=torch.int64, device="cuda")
+            st = torch.zeros(hb.n, dtype=torch.int32, device="cuda")
+            c.reserve(hb.n)
+            bufs.append((hb, db, out, off, st, R.DecodeBuffers(hb.n)))
+        torch.cuda.synchronize()
+        for _ in range(3):
+            for k in (0, 1):                       # enqueue both encodes, then both decodes
+                hb, db, out, off, st, d = bufs[k]
+                codecs[k].encode(db, out, off, st)
+            for k in (0, 1):
+                hb, db, out, off, st, d = bufs[k]
+                codecs[k].decode(out, off, hb.n, L.DECODE_SLICE, d.msgs, d.unix, d.status, d.aux0, d.aux1)
+        torch.cuda.synchronize()
+        for hb, db, out, off, st, d in bufs:
+            o_wire, o_off, o_st, _ = oracle.encode_batch(hb)
+            assert np.array_equal(st.cpu().numpy(), o_st)
+            assert np.array_equal(off.cpu().numpy().view(np.uint64), o_off)
+            assert out[:len(o_wire)].cpu().numpy().tobytes() == o_wire
+            w = np.concatenate([np.frombuffer(o_wire, np.uint8), np.zeros(16, np.uint8)])
+            om, ou, os_, oa0, oa1 = oracle.decode_batch(w, o_off, L.DECODE_SLICE)
+            gm, gu, gs, ga0, ga1 = d.to_host()
+            assert np.array_equal(gs, os_) and np.array_equal(ga0, oa0) and np.array_equal(ga1, oa1)
+            assert np.array_equal(gm.view(np.uint8), om.view(np.uint8))
+            _, gp = L.resolve_unix(gm, gu, gs)
+            _, op = L.resolve_unix(om, ou, os_)
+            assert np.array_equal(gp, op)
+    finally:
+        for c in codecs:
+            c.close()
