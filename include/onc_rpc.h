@@ -387,7 +387,8 @@ int onc_codec_sync(onc_codec* codec);
  * calls into a hipGraph: a call that would grow the scratch while its
  * stream is capturing returns ONC_RC_ECAPTURE (outside a capture the
  * scratch grows on demand with a synchronous hipMalloc). onc_frame_stream
- * keeps its own per-chunk scratch, sized by its first call. */
+ * keeps its own per-chunk scratch, sized by its first call on a stream that
+ * long or longer (growing it inside a capture is ONC_RC_ECAPTURE too). */
 int onc_codec_reserve(onc_codec* codec, uint64_t max_records);
 /* Last HIP error string seen by this handle ("" if none). */
 const char* onc_codec_last_error(const onc_codec* codec);

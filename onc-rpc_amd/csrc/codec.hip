@@ -664,13 +664,19 @@ int onc_frame_stream(onc_codec* c, const uint8_t* wire, uint64_t len, uint64_t* 
                      uint64_t* result) {
     if (!c || !rec_off || !result || (len && !wire)) return ONC_RC_EINVAL;
     if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
-    hipError_t e = hipMemsetAsync(result, 0, 5 * sizeof(uint64_t), c->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
-    if (e != hipSuccess) return fail(c, e, "hipMemsetAsync");
-    if (len == 0 || max_records == 0) return ONC_RC_OK;   // nothing framed, nothing consumed
+    hipError_t e;
+    if (len == 0 || max_records == 0) {                   // nothing framed, nothing consumed
+        e = hipMemsetAsync(result, 0, 5 * sizeof(uint64_t), c->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(rec_off, 0, sizeof(uint64_t), c->stream);
+        if (e != hipSuccess) return fail(c, e, "hipMemsetAsync");
+        return ONC_RC_OK;
+    }
+    // (otherwise frame_guess clears result and rec_off[0] as it starts)
     const uint64_t chunk = c->frame_chunk;
     const uint64_t P = (len + chunk - 1) / chunk;
     if (P > c->frame_chunks) {
+        // (in a capture: frame a stream of this size once before capturing)
+        if (capturing(c)) return refuse_in_capture(c);
         uint64_t want = c->frame_chunks ? c->frame_chunks : 4096;
         while (want < P) want *= 2;
         if (c->frame_scratch) {

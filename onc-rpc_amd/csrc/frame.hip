@@ -170,6 +170,11 @@ __global__ __launch_bounds__(256) void frame_guess_kernel(FrameArgs a) {
         if (f == 0) {
             *a.first_fail = kNone;
             *a.first_stop = kNone;
+            // the call's outputs start cleared (a stream that frames nothing
+            // leaves them so): in this launch instead of two fills
+#pragma unroll
+            for (int k = 0; k < 5; ++k) a.result[k] = 0;
+            a.rec_off[0] = 0;
         }
         if (f < ((a.nchunks + 255) >> 8)) a.fail2[f] = a.stop2[f] = 0;
         if (f < ((a.nchunks + 65535) >> 16)) a.fail3[f] = a.stop3[f] = 0;
