@@ -154,6 +154,8 @@ static void put32(uint8_t* p, uint32_t v) {
 int main(int argc, char** argv) {
     const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 1000000;
     const uint32_t W = argc > 2 ? uint32_t(strtoul(argv[2], 0, 10)) : 300;   // record stride (>= 44)
+    // LAB_UNIX=1: configs[0]-shaped records (W >= 128)
+    const bool unix_cred = getenv("LAB_UNIX") != nullptr && W >= 128;
     std::vector<uint8_t> wire(n * W + 64);
     std::vector<uint64_t> off(n + 1);
     for (uint64_t i = 0; i < n; ++i) {
@@ -162,8 +164,16 @@ int main(int argc, char** argv) {
         put32(p, 0x80000000u | (W - 4));
         put32(p + 4, uint32_t(i));
         put32(p + 8, 0); put32(p + 12, 2); put32(p + 16, 100003); put32(p + 20, 4); put32(p + 24, 1);
-        put32(p + 28, 0); put32(p + 32, 0); put32(p + 36, 0); put32(p + 40, 0);
-        for (uint32_t k = 44; k < W; ++k) p[k] = uint8_t(i * 7 + k);
+        if (unix_cred) {       // configs[0]'s credential: AUTH_UNIX, empty name, 16 gids (128-byte header)
+            put32(p + 28, 1); put32(p + 32, 84); put32(p + 36, uint32_t(i)); put32(p + 40, 0);
+            put32(p + 44, 501); put32(p + 48, 20); put32(p + 52, 16);
+            for (uint32_t g = 0; g < 16; ++g) put32(p + 56 + 4 * g, 100 + g);
+            put32(p + 120, 0); put32(p + 124, 0);
+            for (uint32_t k = 128; k < W; ++k) p[k] = uint8_t(i * 7 + k);
+        } else {
+            put32(p + 28, 0); put32(p + 32, 0); put32(p + 36, 0); put32(p + 40, 0);
+            for (uint32_t k = 44; k < W; ++k) p[k] = uint8_t(i * 7 + k);
+        }
     }
     off[n] = n * W;
     uint8_t* dw; uint64_t* doff; onc_msg* dm; onc_unix_params* du; int32_t* ds; uint32_t *da0, *da1;
@@ -183,7 +193,10 @@ int main(int argc, char** argv) {
     const uint32_t grid = uint32_t((n + 255) / 256);
     struct V { const char* name; std::function<void()> run; std::vector<float> t; };
     std::vector<V> vs = {
-        {"product decode<slice>", [&] { hipLaunchKernelGGL(decode_kernel<ONC_DECODE_SLICE>, dim3(uint32_t((n + kDecTile - 1) / kDecTile)), dim3(kDecTile), 0, 0, a); }, {}},
+        {"product decode<slice>", [&] { hipLaunchKernelGGL((decode_kernel<ONC_DECODE_SLICE, true, true>), dim3(uint32_t((n + kDecTile - 1) / kDecTile)), dim3(kDecTile), 0, 0, a); }, {}},
+        {"product decode<slice, line>", [&] { hipLaunchKernelGGL((decode_kernel<ONC_DECODE_SLICE, true, true, false, false, false, true>), dim3(uint32_t((n + kDecTile - 1) / kDecTile)), dim3(kDecTile), 0, 0, a); }, {}},
+        {"read 8 chunks", [&] { hipLaunchKernelGGL(l_read<8>, dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"read 8 + write", [&] { hipLaunchKernelGGL(l_rw<8>, dim3(grid), dim3(256), 0, 0, a); }, {}},
         {"read 4 chunks", [&] { hipLaunchKernelGGL(l_read<4>, dim3(grid), dim3(256), 0, 0, a); }, {}},
         {"read 3 chunks", [&] { hipLaunchKernelGGL(l_read<3>, dim3(grid), dim3(256), 0, 0, a); }, {}},
         {"read 4 + write", [&] { hipLaunchKernelGGL(l_rw<4>, dim3(grid), dim3(256), 0, 0, a); }, {}},
