@@ -67,7 +67,7 @@ int main(int argc, char** argv) {
         m.verf.kind_len = ONC_AUTH_PACK(ONC_KIND_NONE, 0);
         if (c3) {
             m.cred.id = ONC_AUTH_UNIX;
-            m.cred.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 0);
+            m.cred.kind_len = ONC_AUTH_PACK(ONC_KIND_UNIX, 84);   // declared (ABI 6), as the product's batches
             m.cred.ref = i;
             onc_unix_params& u = unix[i];
             memset(&u, 0, sizeof(u));
@@ -122,7 +122,8 @@ int main(int argc, char** argv) {
         return 1;
     }
     const bool ws = argc > 3 && std::string(argv[3]) == "ws";   // the wave-specialised kernel
-    if (ws) a.ws = 1;
+    if (ws) a.ws = (c3 && !c0) ? 2 : 1;   // the product's long-payload instance for configs[3]
+    a.decl = 1;                            // the plan of an emit (declared AUTH_UNIX lengths as given)
     a.prof = nullptr;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
