@@ -119,6 +119,37 @@ __global__ __launch_bounds__(256) void l_rw(DecArgs a) {
     }
 }
 
+// l_rw with T-thread workgroups (the product decode's are 64)
+template <int NCH, int T>
+__global__ __launch_bounds__(T) void l_rw_t(DecArgs a) {
+    __shared__ uint4 st[T * 4];
+    const int t = threadIdx.x;
+    const uint64_t i0 = uint64_t(blockIdx.x) * T, i = i0 + t;
+    uint4 m[4] = {};
+    if (i < a.n) {
+        const uint64_t b = a.rec_off[i];
+        const uintptr_t win = (reinterpret_cast<uintptr_t>(a.wire) + b) & ~uintptr_t(15);
+        u32x4 v[NCH];
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) v[j] = gload<u32x4>(win + 16 * j);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m[j] = make_uint4(v[j % NCH].x, v[j % NCH].y, uint32_t(b), v[j % NCH].w);
+        __builtin_nontemporal_store(0, a.out.status + i);
+        __builtin_nontemporal_store(0u, a.out.aux0 + i);
+        __builtin_nontemporal_store(0u, a.out.aux1 + i);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st[4 * t + k] = m[k];
+    __syncthreads();
+    const uint64_t nblk = min(uint64_t(T), a.n - i0);
+    u32x4* dst = reinterpret_cast<u32x4*>(a.out.msgs + i0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t j = uint32_t(k * T + t);
+        if (j < 4 * nblk) { const uint4 q = st[j]; __builtin_nontemporal_store(u32x4{q.x, q.y, q.z, q.w}, dst + j); }
+    }
+}
+
 // write-only: descriptors + status/aux
 __global__ __launch_bounds__(256) void l_write(DecArgs a) {
     const uint64_t i0 = uint64_t(blockIdx.x) * 256, i = i0 + threadIdx.x;
@@ -196,6 +227,10 @@ int main(int argc, char** argv) {
         {"product decode<slice>", [&] { hipLaunchKernelGGL((decode_kernel<ONC_DECODE_SLICE, true, true>), dim3(uint32_t((n + kDecTile - 1) / kDecTile)), dim3(kDecTile), 0, 0, a); }, {}},
         {"product decode<slice, line>", [&] { hipLaunchKernelGGL((decode_kernel<ONC_DECODE_SLICE, true, true, false, false, false, true>), dim3(uint32_t((n + kDecTile - 1) / kDecTile)), dim3(kDecTile), 0, 0, a); }, {}},
         {"read 8 chunks", [&] { hipLaunchKernelGGL(l_read<8>, dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"read 8 + nt write, WG 64", [&] { hipLaunchKernelGGL((l_rw_t<8, 64>), dim3(uint32_t((n + 63) / 64)), dim3(64), 0, 0, a); }, {}},
+        {"read 8 + nt write, WG 256", [&] { hipLaunchKernelGGL((l_rw_t<8, 256>), dim3(grid), dim3(256), 0, 0, a); }, {}},
+        {"read 3 + nt write, WG 64", [&] { hipLaunchKernelGGL((l_rw_t<3, 64>), dim3(uint32_t((n + 63) / 64)), dim3(64), 0, 0, a); }, {}},
+        {"read 3 + nt write, WG 256", [&] { hipLaunchKernelGGL((l_rw_t<3, 256>), dim3(grid), dim3(256), 0, 0, a); }, {}},
         {"read 8 + write", [&] { hipLaunchKernelGGL(l_rw<8>, dim3(grid), dim3(256), 0, 0, a); }, {}},
         {"read 4 chunks", [&] { hipLaunchKernelGGL(l_read<4>, dim3(grid), dim3(256), 0, 0, a); }, {}},
         {"read 3 chunks", [&] { hipLaunchKernelGGL(l_read<3>, dim3(grid), dim3(256), 0, 0, a); }, {}},
