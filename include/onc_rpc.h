@@ -16,9 +16,13 @@
  * independent records, executed by hand-written HIP kernels on one GPU.
  *
  * Conventions
- *  - Every pointer marked [dev] is device memory (hipMalloc / torch CUDA
- *    tensor) on the codec's device. Nothing is copied to or from the host by
- *    these calls; all calls are asynchronous on the codec's stream.
+ *  - Every pointer marked [dev] is device-accessible memory on the codec's
+ *    device: device memory (hipMalloc / torch CUDA tensor), or host memory
+ *    mapped for the device (onc_host_register, hipHostMalloc / torch pinned
+ *    memory), which the kernels then read and write in place over PCIe — a
+ *    decode of a socket buffer moves only the header granules it parses.
+ *    Nothing is copied to or from the host by these calls; all calls are
+ *    asynchronous on the codec's stream.
  *  - The caller owns every buffer (the reference never allocates on decode
  *    and reuses caller buffers on encode, README.md:10-14). The codec only
  *    keeps a small scratch area for the record-offset scan.
@@ -55,7 +59,13 @@ extern "C" {
  *    scratch while the stream is being captured (ONC_RC_ECAPTURE); an
  *    AUTH_UNIX onc_auth carries its declared serialised length (kind_len
  *    bits 0..23, written by the decoder; 0 = not declared). */
-#define ONC_RPC_ABI_VERSION 6
+/* 7: a record whose declared AUTH_UNIX credential fails a deferred block
+ *    check keeps its extent with a placeholder header — the record mark of
+ *    the extent, then zeros — instead of zeros alone, so that the stream
+ *    stays framable (onc_encode_iov emits the same placeholder as its header
+ *    iovec); onc_host_register / onc_host_unregister map a caller's host
+ *    buffer (a socket buffer) for the kernels to read and write in place. */
+#define ONC_RPC_ABI_VERSION 7
 
 /* ------------------------------------------------------------------------ */
 /* Wire discriminants (values are the on-wire u32s)                          */
@@ -219,12 +229,19 @@ extern "C" {
  *             serialised length — a mismatch is ONC_ENC_BAD_DESCRIPTOR).
  *             Statuses are the reference order's either way. One placement
  *             difference: a record whose only failure is such a block check
- *             keeps the extent its descriptor declares in the output, its
- *             header bytes zero and its payload in place (every other failing
- *             record takes 0 bytes). onc_encode_lengths reports the same
- *             extents (with every check's status) and onc_encode_iov places
- *             records by them (such a record: no header bytes, zero iovec
- *             lengths); the body roots check every block up front.
+ *             keeps the extent its descriptor declares in the output (every
+ *             other failing record takes 0 bytes), so that the records after
+ *             it stay where the length pass placed them. Its bytes there are a
+ *             placeholder that keeps the stream framable (ABI 7): the record
+ *             mark of the extent, BE32((extent - 4) | 1 << 31) as
+ *             rpc_message.rs:156 writes it — a receiver's expected_message_len
+ *             (:343-367) and onc_frame_stream cut it as one record and go on
+ *             to the next — then zero bytes up to the payload, which is in
+ *             place (a receiver's decode of it fails: InvalidRpcVersion(0)).
+ *             onc_encode_lengths reports the same extents (with every check's
+ *             status) and onc_encode_iov places records by them (such a
+ *             record: its placeholder as the header iovec, its payload
+ *             slice); the body roots check every block up front.
  *  ref      : NONE/SHORT/UNKNOWN: byte offset of the body in the auth arena
  *             (decode: in the wire buffer). UNIX: index into the unix table. */
 typedef struct onc_auth {
@@ -390,6 +407,24 @@ int onc_codec_sync(onc_codec* codec);
  * keeps its own per-chunk scratch, sized by its first call on a stream that
  * long or longer (growing it inside a capture is ONC_RC_ECAPTURE too). */
 int onc_codec_reserve(onc_codec* codec, uint64_t max_records);
+/* Map a caller's host buffer (a socket buffer: any malloc'd or mmap'd
+ * range) for the kernels, so that an encode / decode reads and writes it in
+ * place instead of through a staging copy: pins its pages
+ * (hipHostRegister, mapped and portable) and returns the device address of
+ * `host` in *dev_ptr, usable as any [dev] pointer of this header. The
+ * zero-copy counterpart of the reference's borrowed slices
+ * (call_body.rs:53-59, opaque.rs:92-97): onc_decode of a registered wire
+ * fetches only the 16-byte granules holding the header bytes it parses over
+ * the link, never the payloads. Synchronous. A range already pinned by
+ * hipHostMalloc (or torch's pin_memory) needs no registration: its device
+ * address is returned and nothing is registered (onc_host_unregister of it
+ * is then a no-op). The address is for the codec's device. Returns
+ * ONC_RC_EINVAL for a NULL pointer or length, ONC_RC_EHIP if the runtime
+ * refuses the range (onc_codec_last_error says why). */
+int onc_host_register(onc_codec* codec, void* host, uint64_t len, void** dev_ptr);
+/* Unpin a range onc_host_register pinned (the kernels must be done with it). */
+int onc_host_unregister(onc_codec* codec, void* host);
+
 /* Last HIP error string seen by this handle ("" if none). */
 const char* onc_codec_last_error(const onc_codec* codec);
 const char* onc_status_str(int32_t status);
@@ -455,7 +490,10 @@ int onc_encode_lengths(onc_codec* codec, const onc_batch* batch,
  *   rec_off[dev, n+1]: record i occupies out[rec_off[i], rec_off[i+1]);
  *                      rec_off[n] is the total byte count.
  *   status[dev, n]   : ONC_OK or ONC_ENC_*. Records that fail validation
- *                      occupy 0 bytes. Bytes at or beyond out_cap are never
+ *                      occupy 0 bytes — except a declared AUTH_UNIX record
+ *                      failing only its deferred parameter-block check, which
+ *                      keeps its declared extent as a framable placeholder
+ *                      (onc_auth). Bytes at or beyond out_cap are never
  *                      written; records ending beyond it get ONC_ENC_WRITE_ZERO.
  *   rec_len[dev, n]  : optional (may be NULL) serialised lengths. */
 int onc_encode(onc_codec* codec, const onc_batch* batch,
@@ -493,7 +531,10 @@ int onc_encode_emit(onc_codec* codec, const onc_batch* batch, uint8_t* out, uint
  * and starts at iov[i].wire_off of the equivalent packed send buffer, i.e.
  * the bytes onc_encode would produce, for a writev()/scatter-gather sender.
  *   iov[dev, n]    : one entry per record; all zero lengths for a record
- *                    whose status != ONC_OK.
+ *                    whose status != ONC_OK (except a declared AUTH_UNIX
+ *                    record failing only its deferred block check: its
+ *                    placeholder header and payload slice, as onc_encode
+ *                    writes them, onc_auth).
  *   status[dev, n] : ONC_OK or ONC_ENC_*; a record whose header would end
  *                    beyond hdr_cap gets ONC_ENC_WRITE_ZERO and none of its
  *                    header bytes are written.

@@ -9,6 +9,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -285,8 +287,59 @@ int onc_codec_reserve(onc_codec* c, uint64_t max_records) {
     if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
     const int rc = ensure_scratch(c, onc::num_emit_tiles(max_records));
     if (rc != ONC_RC_OK) return rc;
-    // the plan's record lengths (an encode's chunk at most)
-    return ensure_lens(c, std::min(max_records, c->enc_chunk ? c->enc_chunk : onc::kFusedBlocks * onc::kLenRecs));
+    // the plan's record lengths: onc_encode plans a chunk at a time, but
+    // onc_encode_plan plans the whole batch at once (4 bytes per record)
+    return ensure_lens(c, max_records);
+}
+
+// Host ranges onc_host_register pinned (and may unpin): a range that was
+// already pinned by its owner (hipHostMalloc) is mapped but not recorded.
+static std::mutex g_host_mu;
+static std::set<void*> g_host_pinned;
+
+int onc_host_register(onc_codec* c, void* host, uint64_t len, void** dev_ptr) {
+    if (!c || !host || !len || !dev_ptr) return ONC_RC_EINVAL;
+    *dev_ptr = nullptr;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    // memory the runtime already pinned (hipHostMalloc, a registered range):
+    // only map it (hipHostRegister refuses it)
+    hipPointerAttribute_t attr{};
+    bool pinned = false;
+    if (hipPointerGetAttributes(&attr, host) == hipSuccess) pinned = attr.type == hipMemoryTypeHost;
+    else (void)hipGetLastError();                 // an ordinary host pointer
+    bool mine = false;
+    if (!pinned) {
+        const hipError_t r = hipHostRegister(host, size_t(len), hipHostRegisterMapped | hipHostRegisterPortable);
+        if (r == hipSuccess) {
+            mine = true;
+        } else if (r == hipErrorHostMemoryAlreadyRegistered) {
+            (void)hipGetLastError();
+        } else {
+            (void)hipGetLastError();
+            return fail(c, r, "hipHostRegister");
+        }
+    }
+    hipError_t e;
+    e = hipHostGetDevicePointer(dev_ptr, host, 0);
+    if (e != hipSuccess) {
+        if (mine) (void)hipHostUnregister(host);
+        *dev_ptr = nullptr;
+        return fail(c, e, "hipHostGetDevicePointer");
+    }
+    if (mine) g_host_pinned.insert(host);
+    return ONC_RC_OK;
+}
+
+int onc_host_unregister(onc_codec* c, void* host) {
+    if (!c || !host) return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    const auto it = g_host_pinned.find(host);
+    if (it == g_host_pinned.end()) return ONC_RC_OK;      // not pinned here: nothing to undo
+    g_host_pinned.erase(it);
+    const hipError_t e = hipHostUnregister(host);
+    return e == hipSuccess ? ONC_RC_OK : fail(c, e, "hipHostUnregister");
 }
 
 const char* onc_codec_last_error(const onc_codec* c) { return c ? c->last_error.c_str() : "null codec"; }

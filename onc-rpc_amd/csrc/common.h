@@ -467,6 +467,16 @@ __device__ __forceinline__ void put_header_words(const onc_msg& d, uint32_t len,
     put_header_words(d, len, s, w);
 }
 
+// The header of a record whose declared AUTH_UNIX credential failed a
+// deferred block check (include/onc_rpc.h onc_auth, ABI 7): the record mark
+// of its extent (rpc_message.rs:156), so that a receiver's
+// expected_message_len (:343-367) still frames it, then hw - 1 zero words.
+template <class Sink>
+__device__ __forceinline__ void put_placeholder_words(uint32_t len, uint32_t hw, Sink& out) {
+    out(bswap((len - 4u) | 0x80000000u));
+    for (uint32_t k = 1; k < hw; ++k) out(0u);
+}
+
 // ---------------------------------------------------------------------------
 // Body-level roots (ONC_ROOT_*, include/onc_rpc.h): the serialised_len and
 // serialise_into of one type of the message tree instead of RpcMessage.

@@ -560,23 +560,25 @@ __device__ __forceinline__ void stream_span(const EncArgs& a, const ImgTile& T, 
     }
 }
 
-// A tile whose declared AUTH_UNIX credentials failed their deferred checks
-// (T.bad; rare): once every store of the tile is done, each such record gets
-// its status and its header bytes zeroed in the output (the serialiser wrote
-// an empty parameter block in their place; the payload stays).
-__device__ __forceinline__ void declared_fixup(const EncArgs& a, const ImgTile& T, uint64_t r0, uint64_t T0) {
-    const int lane = threadIdx.x & 63;
-    __builtin_amdgcn_s_waitcnt(0);                    // the tile's stores (same wave) are done
-    if (r0 + lane >= a.n) return;
-    const int32_t st = T.bad[lane];
-    if (st == ONC_OK) return;
-    a.status[r0 + lane] = st;
-    const onc_msg d = a.msgs[r0 + lane];
-    const RecPlan p = plan_record<true>(d, a.unix, a.bounds);       // the extent it was placed with
-    const uint64_t start = a.origin + a.rec_off[r0 + lane];
-    const uint64_t end = min(uint64_t(start + 4ull * meta_hw(p.meta)), a.out_cap);
-    for (uint64_t b = start; b < end; ++b) a.out[b] = 0;
-    (void)T0;
+// A record whose declared AUTH_UNIX credential failed a deferred block check
+// (rare) keeps the extent it was placed with, so that every record after it
+// stays where the plan put it; its header bytes in the image become a
+// placeholder that keeps the stream framable (include/onc_rpc.h onc_auth,
+// ABI 7): the record mark of its extent, (len - 4) | 1 << 31
+// (rpc_message.rs:156: a receiver's expected_message_len, :343-367, cuts it
+// as one whole record and goes on to the next), then zero bytes up to its
+// payload. The header words the serialiser wrote (an empty parameter block
+// in place of the failing one) are cleared first. Leaves the sink at the
+// header's end.
+__device__ __forceinline__ void img_placeholder(uint32_t* img32, ImgSink& w, uint64_t ibb, uint32_t hw, uint64_t len) {
+    const uint32_t b = uint32_t(ibb);
+    img_clear(img32, b, 4u * hw);
+    const uint32_t mark = bswap(uint32_t(len - 4) | 0x80000000u), m = 8u * (b & 3u);
+    __hip_atomic_fetch_or(img32 + img_dword(b >> 2), mark << m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (m) __hip_atomic_fetch_or(img32 + img_dword((b >> 2) + 1), mark >> (32u - m), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WAVEFRONT);
+    w.d = (b >> 2) + hw;
+    w.prev = 0u;
 }
 
 template <int kU, int kNT, bool kFused, bool kRoot = false, bool kGiven = false, bool kPre = false,
@@ -727,12 +729,18 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                 // keeps its extent, the words written so far cleared
                 // (include/onc_rpc.h onc_auth). (Checking the preloaded block
                 // before the header build instead: 15 VGPRs spilled.)
-                // (the status lands in LDS and the record is fixed up when
-                // the tile is done: nothing extra live across the header
-                // build or the stream — 128 VGPRs without spills)
+                // (the status lands in LDS, read back right after the build:
+                // nothing extra live across the header build)
                 DeclCheck dc{a.bounds.auth_len, &T.bad[lane]};
                 if (kRoot) put_root_words(d, uint32_t(len), src, a.root, w);
                 else put_header_words(d, uint32_t(len), src, w, &cq, cred_unix, &dc);
+                if (!kRoot) {
+                    const int32_t bad = T.bad[lane];
+                    if (bad != ONC_OK) {
+                        a.status[r0 + lane] = bad;
+                        img_placeholder(img32, w, ibb, hw, len);
+                    }
+                }
                 if (small) {
                     // all of it lies in non-pure chunks (np = 0): right after
                     // the header (bytes past its end read as zero), by a sink
@@ -776,7 +784,6 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         if (lo_rec == hi_rec && hi_rec == nrec) ONC_PROF(4);
     }
     ONC_PROF(5);
-    if (!kRoot && __any(lane < nrec && T.bad[lane] != ONC_OK)) declared_fixup(a, T, r0, T0);
 }
 
 // ---------------------------------------------------------------------------
@@ -956,9 +963,7 @@ __device__ __forceinline__ void ws_stage_span(const EncArgs& a, WsTile& S, const
             put_header_words(d, uint32_t(Slen), src, w, nullptr, false, &dc);
             if (bad != ONC_OK) {                       // (see enc_emit_tile)
                 a.status[S.r0 + lane] = bad;
-                img_clear(img32, uint32_t(ibb), uint32_t(Spst - Sstart));
-                w.d = uint32_t(ibb >> 2) + uint32_t((Spst - Sstart) >> 2);
-                w.prev = 0u;
+                img_placeholder(img32, w, ibb, uint32_t((Spst - Sstart) >> 2), (Spst - Sstart) + Splen);   // (Slen: not kept live)
             }
             if (small) {
                 const uintptr_t pb = sb + Spst;
@@ -1127,7 +1132,9 @@ __device__ __forceinline__ bool ws_header_heavy(const EncArgs& a) {
     if (!a.block_pay || (a.variant & ONC_VARIANT_WS_PIPELINE)) return false;   // the pipeline on every shape (tests)
     const int lane = threadIdx.x & 63;
     const uint64_t nb = num_len_blocks(a.n);
-    const uint64_t b = uint64_t(lane) * nb / kWsSample;       // strictly increasing while nb >= 64
+    // every workgroup once when there are fewer than kWsSample (lane * nb /
+    // kWsSample would read the head of the launch, some of it twice)
+    const uint64_t b = nb >= kWsSample ? uint64_t(lane) * nb / kWsSample : uint64_t(lane);
     const bool use = uint64_t(lane) < kWsSample && (nb >= kWsSample || uint64_t(lane) < nb);
     const uint64_t pay = use ? a.block_pay[b] : 0;
     const uint64_t all = use ? a.block_sum[b] : 0;

@@ -53,13 +53,14 @@ __global__ __launch_bounds__(kIovLenThreads) void iov_len_kernel(IovArgs a) {
         uint64_t len = 0, hl = 0;
         if (r < a.n) {
             // the extent onc_encode gives the record (declared AUTH_UNIX
-            // lengths), the status of every check; header bytes only for an
-            // OK record (include/onc_rpc.h onc_auth)
+            // lengths) and its header bytes — a record failing only a
+            // deferred block check keeps both, its header a placeholder
+            // (include/onc_rpc.h onc_auth) — with the status of every check
             const onc_msg d = as_msg(mr[k]);
             const RecPlan p = plan_record<true>(d, a.unix, a.bounds);
             const RecPlan f = plan_record<false>(d, a.unix, a.bounds);
             len = p.status == ONC_OK ? p.len : 0;
-            hl = f.status == ONC_OK ? 4ull * meta_hw(f.meta) : 0;
+            hl = p.status == ONC_OK ? 4ull * meta_hw(p.meta) : 0;
             a.status[r] = f.status;
         }
         // header bytes of 64 records < 2^15, so (len << 16 | hl) scans as one u64
@@ -179,14 +180,15 @@ __global__ __launch_bounds__(64 * kIovWaves) void iov_emit_kernel(IovArgs a) {
     uint64_t len = 0, hl = 0;
     bool rec_ok = false;
     if (lane < nrec) {
-        // as iov_len: the extent from the declared lengths, header bytes for
-        // an OK record (iov_len's status: a record failing only a deferred
-        // block check keeps its extent, without header or iovec lengths)
+        // as iov_len: the extent and header bytes from the declared lengths
+        // (a record failing only a deferred block check, iov_len's status
+        // != OK, keeps both: its header is the placeholder onc_encode writes)
         const RecPlan p = plan_record<true>(d, a.unix, a.bounds);
         len = p.status == ONC_OK ? p.len : 0;
-        rec_ok = len != 0 && st0 == ONC_OK;
+        rec_ok = len != 0;
         hl = rec_ok ? 4ull * meta_hw(p.meta) : 0;
     }
+    const bool hole = rec_ok && st0 != ONC_OK;
     const uint64_t sv = (len << 16) | hl;
     const uint64_t incl = wave_incl_scan_u64(sv);
     const uint64_t excl = incl - sv;
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(64 * kIovWaves) void iov_emit_kernel(IovArgs a) {
     const bool fits = hoff + hl <= a.hdr_cap;
     if (lane < nrec) {
         const bool ok = rec_ok && fits;
-        if (rec_ok && !fits) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
+        if (rec_ok && !hole && !fits) a.status[r0 + lane] = ONC_ENC_WRITE_ZERO;
         u32x4* e = reinterpret_cast<u32x4*>(a.iov + r0 + lane);
         const uint64_t po = ok ? d.payload_off : 0;
         const uint32_t pl = ok ? uint32_t(len - hl) : 0u;
@@ -220,7 +222,8 @@ __global__ __launch_bounds__(64 * kIovWaves) void iov_emit_kernel(IovArgs a) {
     if (Ht <= 4ull * kIovHdrCap) {
         if (lane < nrec && hl != 0) {
             PadSink w{hdr, uint32_t((hoff - H0) >> 2)};
-            put_header_words(d, uint32_t(len), src, w);
+            if (hole) put_placeholder_words(uint32_t(len), uint32_t(hl >> 2), w);
+            else put_header_words(d, uint32_t(len), src, w);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -243,7 +246,8 @@ __global__ __launch_bounds__(64 * kIovWaves) void iov_emit_kernel(IovArgs a) {
         // headers beyond the LDS budget (auth bodies near 200 bytes): each
         // record writes its own words
         WordSink w{reinterpret_cast<uint32_t*>(ob) + ((hoff - H0) >> 2)};
-        put_header_words(d, uint32_t(len), src, w);
+        if (hole) put_placeholder_words(uint32_t(len), uint32_t(hl >> 2), w);
+        else put_header_words(d, uint32_t(len), src, w);
     }
 }
 

@@ -8,6 +8,7 @@ missing, and every call that returns a non-zero rc raises.
 from __future__ import annotations
 
 import ctypes as C
+import mmap
 import os
 
 import numpy as np
@@ -23,7 +24,7 @@ K_NAMES = ["enc_len_kernel", "scan_tiles_kernel", "enc_emit_kernel", "decode_ker
            "frame_counts_kernel", "frame_guess_kernel"]
 (K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY, K_IOV_LEN,
  K_IOV_EMIT, K_FRAME, K_FRAME_WRITE, K_FRAME_WALK, K_FRAME_COUNTS, K_FRAME_GUESS) = range(13)
-ABI_VERSION = 6
+ABI_VERSION = 7
 K_COUNT = len(K_NAMES)
 
 # every symbol include/onc_rpc.h declares
@@ -34,7 +35,7 @@ EXPORTED = [
     "onc_kernel_name", "onc_encode_lengths", "onc_encode", "onc_decode", "onc_scan_lengths",
     "onc_expected_message_len", "onc_encode_iov", "onc_frame_stream", "onc_encode_plan", "onc_encode_emit",
     "onc_decode_lengths", "onc_decode_body", "onc_encode_body", "onc_encode_body_lengths",
-    "onc_codec_create_ex", "onc_codec_set_decode_policy",
+    "onc_codec_create_ex", "onc_codec_set_decode_policy", "onc_host_register", "onc_host_unregister",
 ]
 
 # onc_codec_options (include/onc_rpc.h)
@@ -107,6 +108,8 @@ def load_library(path=LIB_PATH):
     lib.onc_decode_body.argtypes = [vp, i32, vp, vp, u64, i32, vp, C.POINTER(OncDecoded), vp]
     lib.onc_encode_body.argtypes = [vp, i32, C.POINTER(OncBatch), vp, u64, vp, vp, vp]
     lib.onc_encode_body_lengths.argtypes = [vp, i32, C.POINTER(OncBatch), vp, vp]
+    lib.onc_host_register.argtypes = [vp, vp, u64, C.POINTER(vp)]
+    lib.onc_host_unregister.argtypes = [vp, vp]
     for name in EXPORTED:
         getattr(lib, name).restype = getattr(lib, name).restype or i32
     # a stale library would read a differently laid out onc_batch and label
@@ -320,6 +323,90 @@ class Codec:
     def scan_lengths(self, rec_len, n, base, rec_off):
         self._check(self.lib.onc_scan_lengths(self.h, _ptr(rec_len), n, base, _ptr(rec_off)),
                     "onc_scan_lengths")
+
+
+class HostMapped:
+    """A host buffer the kernels read and write in place (onc_host_register):
+    page-aligned anonymous memory, as a socket buffer would be. `host` is its
+    numpy byte view (typed views: view(dtype)); data_ptr() is the device
+    address, so it goes wherever a device tensor goes in this binding
+    (Codec calls, DeviceBatch fields). close() unregisters it."""
+
+    def __init__(self, codec: "Codec", nbytes: int):
+        self.nbytes = int(nbytes)
+        self._mm = mmap.mmap(-1, max(self.nbytes, 4096))
+        self.host = np.frombuffer(self._mm, np.uint8, count=self.nbytes)
+        self._addr = self.host.ctypes.data if self.nbytes else np.frombuffer(self._mm, np.uint8).ctypes.data
+        self._codec = codec
+        dev = C.c_void_p()
+        codec._check(codec.lib.onc_host_register(codec.h, C.c_void_p(self._addr), max(self.nbytes, 4096),
+                                                  C.byref(dev)), "onc_host_register")
+        self._dev = dev.value
+
+    @classmethod
+    def from_array(cls, codec, arr):
+        """A mapped copy of a numpy array's bytes."""
+        raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        m = cls(codec, raw.size)
+        m.host[:] = raw
+        return m
+
+    def data_ptr(self):
+        return self._dev
+
+    def numel(self):
+        return self.nbytes
+
+    def element_size(self):
+        return 1
+
+    def view(self, dtype):
+        return self.host.view(dtype)
+
+    def close(self):
+        if self._dev is not None and self._codec.h:
+            self._codec.lib.onc_host_unregister(self._codec.h, C.c_void_p(self._addr))
+        self._dev = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def host_device_pointer(codec: "Codec", t):
+    """Device address of a pinned host tensor (torch pin_memory =
+    hipHostMalloc): onc_host_register maps it without registering it again."""
+    dev = C.c_void_p()
+    codec._check(codec.lib.onc_host_register(codec.h, C.c_void_p(t.data_ptr()), t.numel() * t.element_size(),
+                                             C.byref(dev)), "onc_host_register")
+    return dev.value
+
+
+class MappedHostBatch:
+    """A HostBatch whose arrays live in mapped host memory (HostMapped): an
+    onc_batch the kernels read in place — descriptors, AUTH_UNIX table and
+    arenas never copied to the device."""
+
+    def __init__(self, codec, hb: L.HostBatch):
+        self.n = hb.n
+        self.msgs = HostMapped.from_array(codec, hb.msgs)
+        self.unix = HostMapped.from_array(codec, hb.unix if hb.unix.size else np.zeros(1, L.UNIX_DTYPE))
+        self.auth_arena = HostMapped.from_array(codec, hb.auth_arena if hb.auth_arena.size else np.zeros(16, np.uint8))
+        self.payload_arena = HostMapped.from_array(codec, hb.payload_arena if hb.payload_arena.size
+                                                   else np.zeros(16, np.uint8))
+        self.unix_count = hb.unix.size
+        self.auth_len = hb.auth_arena.size
+        self.payload_len = hb.payload_arena.size
+
+    def c_struct(self):
+        return OncBatch(self.n, self.msgs.data_ptr(), self.unix.data_ptr(), self.auth_arena.data_ptr(),
+                        self.payload_arena.data_ptr(), self.unix_count, self.auth_len, self.payload_len)
+
+    def close(self):
+        for m in (self.msgs, self.unix, self.auth_arena, self.payload_arena):
+            m.close()
 
 
 class DecodeBuffers:

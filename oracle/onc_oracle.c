@@ -926,29 +926,35 @@ int32_t oracle_encode_message(const onc_msg* msg, const onc_unix_params* unix_ta
     return e.code;
 }
 
-/* The library's placement of a record whose AUTH_UNIX auths declare their
- * length (include/onc_rpc.h onc_auth, ABI 6 — the library's own contract,
- * not a reference behaviour): its length pass plans every declared auth from
- * the descriptor alone and checks the parameter blocks only while writing.
- * So a record that fails only a block check (a panic of AuthUnixParams::new /
- * Gids, or declared != serialised length) still takes the extent the
- * descriptor declares: its header bytes zero, its payload (a Call's, an
- * accepted Success's) in place. Only a Call's credential is planned that way
- * (a verifier's block is checked up front). Returns 1 with that extent and
- * header size when every other check passes (encode.hip plan_record<true>). */
+/* The library's placement of a record whose Call credential is an AUTH_UNIX
+ * auth that declares its length (include/onc_rpc.h onc_auth, ABI 6/7 — the
+ * library's own contract, not a reference behaviour): its length pass plans
+ * that credential from the descriptor alone and checks the parameter block
+ * only while writing. So a record whose only failure is that block's check
+ * (a panic of AuthUnixParams::new / Gids, or declared != serialised length)
+ * still takes the extent the descriptor declares: its header is a
+ * placeholder — the record mark of the extent (rpc_message.rs:156), then
+ * zero bytes — and its payload is in place, so the stream stays framable.
+ * Returns 1 with that extent and header size when the credential is such a
+ * declared auth, its block fails, and every check of the declared plan
+ * passes (encode.hip plan_record<true>); else 0 (the record takes no bytes). */
 static int declared_extent(const onc_msg* d, const onc_unix_params* unix_table, uint64_t* len, uint64_t* hdr) {
     /* one auth: serialised_len (id + body) and associated_data_len bound */
     uint64_t aw[2] = {0, 0}, assoc[2] = {0, 0};
     const onc_auth* auths[2] = {&d->cred, &d->verf};
-    const int call = d->msg_type == ONC_MSG_CALL;
-    const int acc = d->msg_type == ONC_MSG_REPLY && d->reply_stat == ONC_REPLY_ACCEPTED;
-    if (!call && !acc) return 0;                      /* no AUTH_UNIX auth: nothing deferred */
-    if (acc && d->stat > ONC_ACCEPT_SYSTEM_ERR) return 0;
-    for (int k = call ? 0 : 1; k < 2; k++) {
+    if (d->msg_type != ONC_MSG_CALL) return 0;       /* only a Call's credential is deferred */
+    if (ONC_AUTH_KIND(d->cred) != ONC_KIND_UNIX || ONC_AUTH_LEN(d->cred) == 0) return 0;
+    {   /* the deferred block check itself must be what fails */
+        const onc_unix_params* p = &unix_table[d->cred.ref];
+        const int bad = p->name_len > ONC_MAX_MACHINE_NAME_LEN || p->ngids > ONC_MAX_GIDS ||
+                        ONC_AUTH_LEN(d->cred) != 20 + 4 * ((p->name_len + 3) / 4) + 4 * p->ngids;
+        if (!bad) return 0;
+    }
+    for (int k = 0; k < 2; k++) {
         const onc_auth* a = auths[k];
         const uint32_t kind = ONC_AUTH_KIND(*a), l = ONC_AUTH_LEN(*a);
         if (kind > ONC_KIND_UNKNOWN) return 0;
-        if (kind == ONC_KIND_UNIX && l != 0 && k == 0) {      /* only a Call's credential is deferred */
+        if (k == 0) {                                 /* the declared credential */
             if (l < 20 || (l & 3) || l > 20 + 4 * 64 + 4 * 16) return 0;   /* implausible */
             aw[k] = 8 + l;
             assoc[k] = l - 8;                         /* > 200 exactly when the true value is */
@@ -963,14 +969,7 @@ static int declared_extent(const onc_msg* d, const onc_unix_params* unix_table, 
             assoc[k] = l;
         }
     }
-    uint64_t h, body;
-    if (call) {
-        h = 28 + aw[0] + aw[1];
-        body = d->payload_len;
-    } else {
-        h = 16 + aw[1] + 4 + (d->stat == ONC_ACCEPT_PROG_MISMATCH ? 8 : 0);
-        body = d->stat == ONC_ACCEPT_SUCCESS ? d->payload_len : 0;
-    }
+    const uint64_t h = 28 + aw[0] + aw[1], body = d->payload_len;
     if ((h + body) & 0xFFFFFFFF80000000ull) return 0;
     if (assoc[0] > ONC_MAX_AUTH_LEN || assoc[1] > ONC_MAX_AUTH_LEN) return 0;
     *len = h + body;
@@ -991,11 +990,14 @@ void oracle_encode_batch(uint64_t n, const onc_msg* msgs, const onc_unix_params*
         uint64_t len = (st == ONC_OK || st == ONC_ENC_WRITE_ZERO) ? slen : 0;
         uint64_t dlen, dhdr;
         if (len == 0 && st != ONC_OK && declared_extent(&msgs[i], unix_table, &dlen, &dhdr)) {
-            /* failed a deferred block check only: the declared extent, header zero, payload copied */
+            /* failed a deferred block check only: the declared extent, the
+             * placeholder header (record mark, zeros), payload copied */
             len = dlen;
             const onc_msg* d = &msgs[i];
+            const uint32_t mark = (uint32_t)(dlen - 4) | 0x80000000u;
             for (uint64_t b = 0; b < dlen && b < cap; b++)
-                out[off + b] = b < dhdr ? 0 : payload_arena[d->payload_off + (b - dhdr)];
+                out[off + b] = b < 4 ? (uint8_t)(mark >> (24 - 8 * b))
+                                     : b < dhdr ? 0 : payload_arena[d->payload_off + (b - dhdr)];
         }
         if (rec_off) rec_off[i] = off;
         if (status) status[i] = st;

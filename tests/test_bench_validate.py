@@ -84,3 +84,44 @@ def test_validate_iov_rejects(oracle, corrupt):
     else:
         t["iov_tot"][1] += 1
     assert not _validate(_bench(), t)
+
+
+def test_iov_gather_ok_rebuilds_the_wire(oracle):
+    """bench.iov_gather_ok (the host-side check of the PCIe-inclusive
+    vectored legs): the writev gather of header slices + host payload slices
+    equals the oracle's wire, in steps smaller than the batch; a wrong header
+    byte, payload offset or wire offset is caught."""
+    import onc_rpc_amd.layout as L
+    bm = _bench()
+    t = _case(oracle)
+    e = t["iov"].numpy().view(L.IOV_DTYPE).copy()
+    hdr = t["hdr_out"].numpy()
+    pay = t["hb"].payload_arena
+    ref = t["wire"].numpy()
+    assert bm.iov_gather_ok(hdr, e, pay, ref, step=777)
+    h2 = hdr.copy()
+    h2[t["hdr_total"] // 3] ^= 4
+    assert not bm.iov_gather_ok(h2, e, pay, ref, step=777)
+    e2 = e.copy()
+    e2["payload_off"][100] += 1
+    assert not bm.iov_gather_ok(hdr, e2, pay, ref)
+    e3 = e.copy()
+    e3["wire_off"][50] += 4
+    assert not bm.iov_gather_ok(hdr, e3, pay, ref)
+    # a chunk of it against its slice of the wire (the pipelined leg's check)
+    lo, hi = 1000, 2000
+    w0, w1 = int(e["wire_off"][lo]), int(e["wire_off"][hi])
+    ec = e[lo:hi].copy()
+    ec["wire_off"] -= w0
+    assert bm.iov_gather_ok(hdr, ec, pay, ref[w0:w1])
+
+
+def test_parsed_lines_bytes():
+    """The line count of the zero-copy decode's note: records of 300 bytes
+    packed from 0 — a record's first 48 bytes span two 128-byte lines when
+    they cross a line boundary."""
+    bm = _bench()
+    lens = np.full(8, 300, np.int64)
+    starts = np.arange(8) * 300
+    want = sum(((s + 47) // 128 - s // 128 + 1) * 128 for s in starts)
+    assert bm.parsed_lines_bytes(lens) == want

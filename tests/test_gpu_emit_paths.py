@@ -237,7 +237,8 @@ def _adversarial(seed, n=3000):
 @pytest.mark.parametrize("seed", [71, 72])
 def test_declared_lengths_broken_blocks(codec, R, oracle, seed):
     """Records whose only failure is a deferred block check keep the extent
-    their descriptor declares (header bytes zero, payload in place) with the
+    their descriptor declares (a placeholder header: the record mark of the
+    extent, then zeros — ABI 7; payload in place) with the
     check's status; the others get the full plan's reference-order status
     and no bytes — the oracle's restatement of the rule, bit-exact, at two
     writer positions and with a capacity inside the batch. onc_encode_lengths

@@ -131,9 +131,10 @@ def test_iov_declared_extents(codec, R, oracle):
     (tests/test_gpu_emit_paths.py::_adversarial): the vectored encode places
     records as onc_encode does (wire_off = the oracle's offsets for every
     record, a failing record's declared extent included; totals[1] = the
-    packed total), the statuses are the oracle's, a failing record has zero
-    header and payload lengths, and every OK record's header bytes and
-    payload slice are the oracle's."""
+    packed total), the statuses are the oracle's, a record that fails without
+    an extent has zero lengths, and every record with an extent — a failing
+    declared one's placeholder header (ABI 7) included — gathers to the
+    oracle's bytes: its header slice, then its payload slice."""
     from test_gpu_emit_paths import _adversarial
     hb = _adversarial(75, n=2500)
     o_wire, o_off, o_st, o_len = oracle.encode_batch(hb)
@@ -142,10 +143,10 @@ def test_iov_declared_extents(codec, R, oracle):
     assert np.array_equal(st, o_st)
     assert np.array_equal(iov["wire_off"], o_off[:-1])
     assert int(tot[1]) == int(o_off[-1])
-    ok = st == 0
-    assert (iov["hdr_len"][~ok] == 0).all() and (iov["payload_len"][~ok] == 0).all()
+    gone = o_len == 0
+    assert (iov["hdr_len"][gone] == 0).all() and (iov["payload_len"][gone] == 0).all()
     w = np.frombuffer(o_wire, np.uint8)
-    for i in np.nonzero(ok)[0]:
+    for i in np.nonzero(~gone)[0]:
         e = iov[i]
         a, hl, pl = int(o_off[i]), int(e["hdr_len"]), int(e["payload_len"])
         assert hl + pl == int(o_len[i])

@@ -248,3 +248,53 @@ def test_assoc_200_encodes_but_wire_208_fails_decode(oracle):
     assert st == 0
     for mode in (L.DECODE_SLICE, L.DECODE_BYTES):
         assert oracle.decode_message(out, mode)[0] == 10
+
+
+def test_declared_extent_placeholder(oracle):
+    """The library's placement rule for a declared AUTH_UNIX credential whose
+    deferred block check fails (include/onc_rpc.h onc_auth, ABI 7), as the
+    oracle restates it: the record keeps its declared extent and its header
+    is a placeholder — the record mark of the extent (rpc_message.rs:156),
+    then zeros — followed by its payload, so the serial
+    expected_message_len loop (rpc_message.rs:343-367) frames every record
+    and the placeholder decodes to InvalidRpcVersion(0). Records failing any
+    other way (a verifier over 200 bytes next to the broken block, an
+    undeclared broken credential, a broken AUTH_UNIX verifier of an accepted
+    reply) take no bytes."""
+    unix = {"kind": "unix", "stamp": 7, "machine_name": b"host".hex(), "uid": 1, "gid": 2, "gids": [3, 4, 5]}
+    none = {"kind": "none"}
+
+    def call(xid, cred, verf=none, payload=b"\x11" * 10):
+        return {"xid": xid, "type": "call", "program": 100003, "program_version": 4, "procedure": 1,
+                "cred": cred, "verf": verf, "payload": payload.hex()}
+    msgs = [call(1, unix), call(2, unix), call(3, unix, {"kind": "short", "data": ("ab" * 201)}),
+            call(4, unix), call(5, none),
+            {"xid": 6, "type": "reply", "reply": "accepted", "verf": unix, "accept_status": "success",
+             "payload": "22" * 5},
+            call(7, none)]
+    hb = L.build_batch(msgs, declare=True)
+    m = hb.msgs
+    ref = lambda i, f="cred": int(m[f + "_ref"][i])          # noqa: E731
+    hb.unix["ngids"][ref(1)] = 17                             # broken block, declared: placeholder
+    hb.unix["ngids"][ref(2)] = 17                             # broken block + verifier > 200: no bytes
+    m["cred_kind_len"][3] = int(L.pack_kind_len(L.KIND_UNIX, 0))
+    hb.unix["ngids"][ref(3)] = 17                             # undeclared broken block: no bytes
+    hb.unix["name_len"][ref(5, "verf")] = 300                 # a reply's verifier is checked up front
+    wire, off, st, ln = oracle.encode_batch(hb)
+    assert list(st) == [0, 103, 103, 103, 0, 102, 0]          # the construction panic before the assert
+    decl = L.unix_body_len(4, 3)
+    ext = 4 + 4 + 4 + 16 + (8 + decl) + 8 + 10
+    assert list(ln[[1, 2, 3, 5]]) == [ext, 0, 0, 0]
+    w = np.frombuffer(wire, np.uint8)
+    a = int(off[1])
+    hole = w[a:a + ext].tobytes()
+    assert hole[:4] == ((ext - 4) | 0x80000000).to_bytes(4, "big")
+    assert hole[4:ext - 10] == bytes(ext - 14) and hole[ext - 10:] == b"\x11" * 10
+    # framable: every record with an extent, in order
+    fo, n, consumed, fst = oracle.frame_stream(wire)[:4]
+    has = ln != 0
+    assert (n, consumed, fst) == (int(has.sum()), len(wire), 0)
+    assert np.array_equal(fo[:-1], off[:-1][has])
+    ms, _, ss, a0, _ = oracle.decode_batch(np.frombuffer(wire + b"\0" * 16, np.uint8), fo, L.DECODE_SLICE)
+    assert list(ss) == [0, 11, 0, 0] and int(a0[1]) == 0      # the placeholder: InvalidRpcVersion(0)
+    assert list(ms["xid"][[0, 2, 3]]) == [1, 5, 7]
