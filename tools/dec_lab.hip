@@ -187,11 +187,22 @@ int main(int argc, char** argv) {
     const uint32_t W = argc > 2 ? uint32_t(strtoul(argv[2], 0, 10)) : 300;   // record stride (>= 44)
     // LAB_UNIX=1: configs[0]-shaped records (W >= 128)
     const bool unix_cred = getenv("LAB_UNIX") != nullptr && W >= 128;
-    std::vector<uint8_t> wire(n * W + 64);
+    // LAB_VAR=lo,hi: record lengths uniform in [lo, hi] (configs[2]'s spacing: AUTH_NONE calls of
+    // 64..4096-byte payloads, ~2 KB apart) instead of a fixed W
+    uint32_t vlo = W, vhi = W;
+    if (getenv("LAB_VAR")) sscanf(getenv("LAB_VAR"), "%u,%u", &vlo, &vhi);
     std::vector<uint64_t> off(n + 1);
+    uint64_t x = 88172645463325252ull, tot = 0;
     for (uint64_t i = 0; i < n; ++i) {
-        uint8_t* p = &wire[i * W];
-        off[i] = i * W;
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        off[i] = tot;
+        tot += vlo + (vhi > vlo ? x % (vhi - vlo + 1) : 0);
+    }
+    off[n] = tot;
+    std::vector<uint8_t> wire(tot + 64);
+    for (uint64_t i = 0; i < n; ++i) {
+        uint8_t* p = &wire[off[i]];
+        const uint32_t W = uint32_t(off[i + 1] - off[i]);
         put32(p, 0x80000000u | (W - 4));
         put32(p + 4, uint32_t(i));
         put32(p + 8, 0); put32(p + 12, 2); put32(p + 16, 100003); put32(p + 20, 4); put32(p + 24, 1);
@@ -206,7 +217,6 @@ int main(int argc, char** argv) {
             for (uint32_t k = 44; k < W; ++k) p[k] = uint8_t(i * 7 + k);
         }
     }
-    off[n] = n * W;
     uint8_t* dw; uint64_t* doff; onc_msg* dm; onc_unix_params* du; int32_t* ds; uint32_t *da0, *da1;
     CK(hipMalloc(&dw, wire.size()));
     CK(hipMalloc(&doff, 8 * (n + 1)));
