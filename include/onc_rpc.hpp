@@ -27,9 +27,12 @@
 //
 // All codec work runs on the GPU through libonc_rpc_amd.so:
 //   BatchEncoder  — the caller's serialise_into loop over many messages,
-//                   one onc_encode launch (plus the H2D/D2H copies).
+//                   one onc_encode_body call (one pass, no length pass).
 //   BatchDecoder  — the caller's try_from loop over many records, one
-//                   onc_decode launch.
+//                   onc_decode_lengths call.
+//   Both stage their inputs and outputs in the codec's mapped pinned host
+//   memory (Codec::stage): the kernels read and write it in place over PCIe
+//   — no device allocation and no copy calls, one synchronisation per call.
 //   RpcMessage::serialise_into / serialised_len / try_from — single-message
 //                   forms, implemented as batches of one (for API parity;
 //                   use the batch classes for throughput).
@@ -438,7 +441,11 @@ public:
         if (onc_codec_create(&h_, device, stream) != ONC_RC_OK) throw CodecError("onc_codec_create failed");
     }
     ~Codec() {
-        if (h_) onc_codec_destroy(h_);
+        if (h_) {
+            (void)onc_codec_sync(h_);
+            onc_codec_destroy(h_);
+        }
+        if (stage_host_) (void)hipHostFree(stage_host_);
     }
     Codec(const Codec&) = delete;
     Codec& operator=(const Codec&) = delete;
@@ -448,8 +455,48 @@ public:
     }
     void sync() const { check(onc_codec_sync(h_), "onc_codec_sync"); }
 
+    // The mirror's staging area: mapped pinned host memory (hipHostMalloc,
+    // hipHostMallocMapped). Every BatchEncoder / BatchDecoder call (and so
+    // every single-message form) puts its inputs there and points the
+    // kernels' outputs there, so the kernels read and write it in place over
+    // PCIe (include/onc_rpc.h ABI 7: a [dev] pointer may be mapped host
+    // memory) — no device allocation, no copy calls, one stream
+    // synchronisation per call. `host` and `dev` address the same bytes;
+    // valid until the next stage() call on this codec (every mirror call
+    // synchronises before it returns).
+    struct Stage {
+        uint8_t* host;
+        uint8_t* dev;
+    };
+    Stage stage(size_t n) {
+        if (n > stage_cap_) {
+            size_t want = stage_cap_ ? stage_cap_ : (size_t(1) << 20);
+            while (want < n) want *= 2;
+            if (stage_host_) {
+                sync();
+                (void)hipHostFree(stage_host_);
+                stage_host_ = stage_dev_ = nullptr;
+                stage_cap_ = 0;
+            }
+            void* h = nullptr;
+            if (hipHostMalloc(&h, want, hipHostMallocMapped) != hipSuccess) throw CodecError("hipHostMalloc(stage)");
+            void* d = nullptr;
+            if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+                (void)hipHostFree(h);
+                throw CodecError("hipHostGetDevicePointer(stage)");
+            }
+            stage_host_ = static_cast<uint8_t*>(h);
+            stage_dev_ = static_cast<uint8_t*>(d);
+            stage_cap_ = want;
+        }
+        return Stage{stage_host_, stage_dev_};
+    }
+
 private:
     onc_codec* h_ = nullptr;
+    uint8_t* stage_host_ = nullptr;
+    uint8_t* stage_dev_ = nullptr;
+    size_t stage_cap_ = 0;
 };
 
 namespace detail {
@@ -458,32 +505,26 @@ inline void hip_check(hipError_t e, const char* what) {
     if (e != hipSuccess) throw CodecError(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Device buffer (bytes), grown on demand.
-class DevBuf {
-public:
-    DevBuf() = default;
-    ~DevBuf() {
-        if (p_) (void)hipFree(p_);
-    }
-    DevBuf(const DevBuf&) = delete;
-    DevBuf& operator=(const DevBuf&) = delete;
-    void* ensure(size_t n) {
-        if (n == 0) n = 16;
-        if (n > cap_) {
-            if (p_) hip_check(hipFree(p_), "hipFree");
-            p_ = nullptr;
-            hip_check(hipMalloc(&p_, n), "hipMalloc");
-            cap_ = n;
-        }
-        return p_;
-    }
-    template <class T>
-    T* as() const { return static_cast<T*>(p_); }
-
-private:
-    void* p_ = nullptr;
-    size_t cap_ = 0;
+// Typed regions of a staging area (256-byte aligned): sized first with
+// need(), then taken in the same order from the codec's stage.
+inline size_t rounded(size_t b) { return (b + 255) & ~size_t(255); }
+template <class T>
+struct Region {
+    T* host;
+    T* dev;
 };
+struct Carve {
+    Codec::Stage s;
+    size_t off = 0;
+    template <class T>
+    Region<T> take(size_t count) {
+        const size_t a = off;
+        off += rounded(count * sizeof(T) + 16);
+        return Region<T>{reinterpret_cast<T*>(s.host + a), reinterpret_cast<T*>(s.dev + a)};
+    }
+};
+template <class T>
+inline size_t need(size_t count) { return rounded(count * sizeof(T) + 16); }
 
 }  // namespace detail
 
@@ -499,9 +540,9 @@ public:
     const ReplyBody* reply_body() const { return message_.reply_body(); }
     bool operator==(const RpcMessage& o) const { return xid_ == o.xid_ && message_ == o.message_; }
 
-    // Single-message calls: each is a whole GPU round trip (the message's
-    // descriptor and arenas copied to the device, the kernels, the results
-    // copied back, a stream synchronisation) — tens of microseconds where the
+    // Single-message calls: each is a whole GPU round trip (the message
+    // staged in mapped host memory, the kernels reading and writing it in
+    // place, a stream synchronisation) — tens of microseconds where the
     // reference's CPU call takes ~100 ns (tests/cpp/test_mirror.cpp
     // test_single_message_cost prints both). They exist for tests and tiny
     // batches; a caller with many messages uses BatchEncoder / BatchDecoder
@@ -578,7 +619,10 @@ public:
     std::vector<uint32_t> serialised_lens(Codec& codec, std::vector<int32_t>* status = nullptr);
 
 private:
-    void upload(onc_batch& b);
+    // the batch's descriptors, AUTH_UNIX table and arenas copied into the
+    // codec's mapped staging (the kernels read them there in place)
+    size_t staged_bytes() const;
+    onc_batch stage_batch(detail::Carve& c) const;
     void put_auth(const AuthFlavor& a, onc_auth& d);
     void put_payload(Bytes p, onc_msg& d);
     void put_call(const CallBody& c, onc_msg& d);
@@ -593,7 +637,6 @@ private:
     std::vector<onc_msg> msgs_;
     std::vector<onc_unix_params> unix_;
     std::vector<uint8_t> auth_, payload_;
-    detail::DevBuf d_msgs_, d_unix_, d_auth_, d_payload_, d_out_, d_off_, d_status_, d_len_;
 };
 
 // Result of decoding one record (Result<RpcMessage<&[u8], &[u8]>, Error>).
@@ -627,9 +670,17 @@ public:
                                          std::optional<Error>* stop = nullptr);
 
 private:
-    std::vector<Decoded> decode_device(Codec& codec, const uint8_t* wire, const uint8_t* dw, size_t n,
-                                       const uint64_t* doff, DecodeMode mode);
-    detail::DevBuf d_wire_, d_len_, d_off_, d_msgs_, d_unix_, d_status_, d_aux0_, d_aux1_, d_res_;
+    // the decode outputs in staging regions, read after the synchronisation
+    struct Out {
+        detail::Region<onc_msg> msgs;
+        detail::Region<onc_unix_params> unix;
+        detail::Region<int32_t> status;
+        detail::Region<uint32_t> aux0, aux1;
+        onc_decoded dev() const { return onc_decoded{msgs.dev, unix.dev, status.dev, aux0.dev, aux1.dev}; }
+    };
+    static size_t out_bytes(size_t n);
+    static Out take_out(detail::Carve& c, size_t n);
+    static std::vector<Decoded> results(const Out& o, size_t n, const uint8_t* wire);
 };
 
 // expected_message_len (rpc_message.rs:343-367); throws Error.
@@ -818,67 +869,78 @@ inline void BatchEncoder::push(const AuthUnixParams& p) {
     msgs_.push_back(d);
 }
 
-inline void BatchEncoder::upload(onc_batch& b) {
-    using detail::hip_check;
+inline size_t BatchEncoder::staged_bytes() const {
+    using detail::need;
+    return need<onc_msg>(msgs_.size()) + need<onc_unix_params>(unix_.size()) + need<uint8_t>(auth_.size()) +
+           need<uint8_t>(payload_.size());
+}
+
+inline onc_batch BatchEncoder::stage_batch(detail::Carve& c) const {
     const size_t n = msgs_.size();
+    const auto m = c.take<onc_msg>(n);
+    const auto u = c.take<onc_unix_params>(unix_.size());
+    const auto a = c.take<uint8_t>(auth_.size());
+    const auto p = c.take<uint8_t>(payload_.size());
+    if (n) std::memcpy(m.host, msgs_.data(), n * sizeof(onc_msg));
+    if (!unix_.empty()) std::memcpy(u.host, unix_.data(), unix_.size() * sizeof(onc_unix_params));
+    if (!auth_.empty()) std::memcpy(a.host, auth_.data(), auth_.size());
+    if (!payload_.empty()) std::memcpy(p.host, payload_.data(), payload_.size());
+    onc_batch b{};
     b.n = n;
-    b.msgs = static_cast<const onc_msg*>(d_msgs_.ensure(n * sizeof(onc_msg)));
-    b.unix_params = static_cast<const onc_unix_params*>(d_unix_.ensure(unix_.size() * sizeof(onc_unix_params)));
-    b.auth_arena = static_cast<const uint8_t*>(d_auth_.ensure(auth_.size() + 16));
-    b.payload_arena = static_cast<const uint8_t*>(d_payload_.ensure(payload_.size() + 16));
+    b.msgs = m.dev;
+    b.unix_params = u.dev;
+    b.auth_arena = a.dev;
+    b.payload_arena = p.dev;
     b.unix_count = unix_.size();
     b.auth_len = auth_.size();
     b.payload_len = payload_.size();
-    if (n) hip_check(hipMemcpy(d_msgs_.as<void>(), msgs_.data(), n * sizeof(onc_msg), hipMemcpyHostToDevice), "H2D");
-    if (!unix_.empty())
-        hip_check(hipMemcpy(d_unix_.as<void>(), unix_.data(), unix_.size() * sizeof(onc_unix_params),
-                            hipMemcpyHostToDevice), "H2D");
-    if (!auth_.empty())
-        hip_check(hipMemcpy(d_auth_.as<void>(), auth_.data(), auth_.size(), hipMemcpyHostToDevice), "H2D");
-    if (!payload_.empty())
-        hip_check(hipMemcpy(d_payload_.as<void>(), payload_.data(), payload_.size(), hipMemcpyHostToDevice), "H2D");
+    return b;
 }
 
 inline std::vector<uint32_t> BatchEncoder::serialised_lens(Codec& codec, std::vector<int32_t>* status) {
+    using detail::need;
     const size_t n = msgs_.size();
     std::vector<uint32_t> lens(n);
     std::vector<int32_t> st(n);
     if (n) {
-        onc_batch b{};
-        upload(b);
-        uint32_t* dl = static_cast<uint32_t*>(d_len_.ensure(n * 4));
-        int32_t* ds = static_cast<int32_t*>(d_status_.ensure(n * 4));
-        codec.check(onc_encode_body_lengths(codec.get(), root(), &b, dl, ds), "onc_encode_body_lengths");
+        detail::Carve c{codec.stage(staged_bytes() + need<uint32_t>(n) + need<int32_t>(n))};
+        const onc_batch b = stage_batch(c);
+        const auto dl = c.take<uint32_t>(n);
+        const auto ds = c.take<int32_t>(n);
+        codec.check(onc_encode_body_lengths(codec.get(), root(), &b, dl.dev, ds.dev), "onc_encode_body_lengths");
         codec.sync();
-        detail::hip_check(hipMemcpy(lens.data(), dl, n * 4, hipMemcpyDeviceToHost), "D2H");
-        detail::hip_check(hipMemcpy(st.data(), ds, n * 4, hipMemcpyDeviceToHost), "D2H");
+        std::memcpy(lens.data(), dl.host, n * 4);
+        std::memcpy(st.data(), ds.host, n * 4);
     }
     if (status) *status = std::move(st);
     return lens;
 }
 
+// One encode pass: the output goes into the stage with a capacity no record
+// can reach (a header is at most 460 bytes — 7 words and two auths of 54 —
+// and a record keeping a declared extent at most 28 + 2 x 348 bytes before
+// its payload), so no separate length pass is needed to size it; the bytes
+// are then appended to `out`.
 inline std::vector<int32_t> BatchEncoder::serialise_into(Codec& codec, std::vector<uint8_t>& out,
                                                          std::vector<uint64_t>* rec_off) {
+    using detail::need;
     const size_t n = msgs_.size();
     std::vector<int32_t> st(n);
     std::vector<uint64_t> off(n + 1, 0);
     if (n) {
-        // Size pass (lengths kernel), then the encode into an exact buffer.
-        const std::vector<uint32_t> lens = serialised_lens(codec);
-        uint64_t total = 0;
-        for (uint32_t l : lens) total += l;
-        onc_batch b{};
-        upload(b);
-        uint8_t* dout = static_cast<uint8_t*>(d_out_.ensure(total + 16));
-        uint64_t* doff = static_cast<uint64_t*>(d_off_.ensure((n + 1) * 8));
-        int32_t* ds = static_cast<int32_t*>(d_status_.ensure(n * 4));
-        codec.check(onc_encode_body(codec.get(), root(), &b, dout, total, doff, ds, nullptr), "onc_encode_body");
+        const size_t cap = 1024 * n + payload_.size();
+        detail::Carve c{codec.stage(staged_bytes() + need<uint8_t>(cap) + need<uint64_t>(n + 1) + need<int32_t>(n))};
+        const onc_batch b = stage_batch(c);
+        const auto dout = c.take<uint8_t>(cap);
+        const auto doff = c.take<uint64_t>(n + 1);
+        const auto ds = c.take<int32_t>(n);
+        codec.check(onc_encode_body(codec.get(), root(), &b, dout.dev, cap, doff.dev, ds.dev, nullptr),
+                    "onc_encode_body");
         codec.sync();
-        const size_t base = out.size();
-        out.resize(base + total);
-        if (total) detail::hip_check(hipMemcpy(out.data() + base, dout, total, hipMemcpyDeviceToHost), "D2H");
-        detail::hip_check(hipMemcpy(st.data(), ds, n * 4, hipMemcpyDeviceToHost), "D2H");
-        detail::hip_check(hipMemcpy(off.data(), doff, (n + 1) * 8, hipMemcpyDeviceToHost), "D2H");
+        std::memcpy(st.data(), ds.host, n * 4);
+        std::memcpy(off.data(), doff.host, (n + 1) * 8);
+        const uint64_t total = off[n];
+        out.insert(out.end(), dout.host, dout.host + total);
     }
     if (rec_off) *rec_off = std::move(off);
     return st;
@@ -928,70 +990,81 @@ inline RpcMessage message_view(const onc_msg& d, const onc_unix_params* unix, co
 
 }  // namespace detail
 
-inline std::vector<Decoded> BatchDecoder::decode_device(Codec& codec, const uint8_t* wire, const uint8_t* dw,
-                                                        size_t n, const uint64_t* doff, DecodeMode mode) {
-    using detail::hip_check;
+inline size_t BatchDecoder::out_bytes(size_t n) {
+    using detail::need;
+    return need<onc_msg>(n) + need<onc_unix_params>(2 * n) + need<int32_t>(n) + 2 * need<uint32_t>(n);
+}
+
+inline BatchDecoder::Out BatchDecoder::take_out(detail::Carve& c, size_t n) {
+    Out o;
+    o.msgs = c.take<onc_msg>(n);
+    o.unix = c.take<onc_unix_params>(2 * n);
+    o.status = c.take<int32_t>(n);
+    o.aux0 = c.take<uint32_t>(n);
+    o.aux1 = c.take<uint32_t>(n);
+    return o;
+}
+
+// Descriptors -> RpcMessage views over the caller's `wire` (offsets in the
+// descriptors are relative to the decoded buffer, the same bytes).
+inline std::vector<Decoded> BatchDecoder::results(const Out& o, size_t n, const uint8_t* wire) {
     std::vector<Decoded> res(n);
-    if (!n) return res;
-    onc_decoded out{};
-    out.msgs = static_cast<onc_msg*>(d_msgs_.ensure(n * sizeof(onc_msg)));
-    out.unix_params = static_cast<onc_unix_params*>(d_unix_.ensure(2 * n * sizeof(onc_unix_params)));
-    out.status = static_cast<int32_t*>(d_status_.ensure(n * 4));
-    out.aux0 = static_cast<uint32_t*>(d_aux0_.ensure(n * 4));
-    out.aux1 = static_cast<uint32_t*>(d_aux1_.ensure(n * 4));
-    codec.check(onc_decode(codec.get(), dw, doff, n, int(mode), &out), "onc_decode");
-    codec.sync();
-    std::vector<onc_msg> msgs(n);
-    std::vector<onc_unix_params> unix(2 * n);
-    std::vector<int32_t> st(n);
-    std::vector<uint32_t> a0(n), a1(n);
-    hip_check(hipMemcpy(msgs.data(), out.msgs, n * sizeof(onc_msg), hipMemcpyDeviceToHost), "D2H");
-    hip_check(hipMemcpy(unix.data(), out.unix_params, 2 * n * sizeof(onc_unix_params), hipMemcpyDeviceToHost), "D2H");
-    hip_check(hipMemcpy(st.data(), out.status, n * 4, hipMemcpyDeviceToHost), "D2H");
-    hip_check(hipMemcpy(a0.data(), out.aux0, n * 4, hipMemcpyDeviceToHost), "D2H");
-    hip_check(hipMemcpy(a1.data(), out.aux1, n * 4, hipMemcpyDeviceToHost), "D2H");
     for (size_t i = 0; i < n; ++i) {
-        res[i].status = st[i];
-        res[i].aux0 = a0[i];
-        res[i].aux1 = a1[i];
-        if (st[i] == ONC_OK) res[i].message = detail::message_view(msgs[i], unix.data(), wire);
+        res[i].status = o.status.host[i];
+        res[i].aux0 = o.aux0.host[i];
+        res[i].aux1 = o.aux1.host[i];
+        if (res[i].status == ONC_OK) res[i].message = detail::message_view(o.msgs.host[i], o.unix.host, wire);
     }
     return res;
 }
 
+// The wire is copied into the stage (the caller's buffer is not pinned) and
+// decoded there in place by onc_decode_lengths (offsets inside the decode:
+// one pass); the outputs land in the stage.
 inline std::vector<Decoded> BatchDecoder::try_from(Codec& codec, const uint8_t* wire, size_t wire_len,
                                                    const std::vector<uint32_t>& rec_len, DecodeMode mode) {
-    using detail::hip_check;
+    using detail::need;
     const size_t n = rec_len.size();
     if (!n) return {};
-    uint8_t* dw = static_cast<uint8_t*>(d_wire_.ensure(wire_len + 16));
-    if (wire_len) hip_check(hipMemcpy(dw, wire, wire_len, hipMemcpyHostToDevice), "H2D");
-    uint32_t* dl = static_cast<uint32_t*>(d_len_.ensure(n * 4));
-    hip_check(hipMemcpy(dl, rec_len.data(), n * 4, hipMemcpyHostToDevice), "H2D");
-    uint64_t* doff = static_cast<uint64_t*>(d_off_.ensure((n + 1) * 8));
-    codec.check(onc_scan_lengths(codec.get(), dl, n, 0, doff), "onc_scan_lengths");
-    return decode_device(codec, wire, dw, n, doff, mode);
+    detail::Carve c{codec.stage(need<uint8_t>(wire_len) + need<uint32_t>(n) + out_bytes(n))};
+    const auto w = c.take<uint8_t>(wire_len);
+    const auto l = c.take<uint32_t>(n);
+    if (wire_len) std::memcpy(w.host, wire, wire_len);
+    std::memcpy(l.host, rec_len.data(), n * 4);
+    const Out o = take_out(c, n);
+    const onc_decoded d = o.dev();
+    codec.check(onc_decode_lengths(codec.get(), w.dev, l.dev, n, 0, int(mode), nullptr, &d), "onc_decode_lengths");
+    codec.sync();
+    return results(o, n, wire);
 }
 
 inline std::vector<Decoded> BatchDecoder::try_from_stream(Codec& codec, const uint8_t* wire, size_t wire_len,
                                                           DecodeMode mode, size_t* consumed,
                                                           std::optional<Error>* stop) {
-    using detail::hip_check;
-    uint8_t* dw = static_cast<uint8_t*>(d_wire_.ensure(wire_len + 16));
-    if (wire_len) hip_check(hipMemcpy(dw, wire, wire_len, hipMemcpyHostToDevice), "H2D");
+    using detail::need;
     const size_t max_records = wire_len / 4 + 1;   // every record is at least 4 bytes
-    uint64_t* doff = static_cast<uint64_t*>(d_off_.ensure((max_records + 1) * 8));
-    uint64_t* dres = static_cast<uint64_t*>(d_res_.ensure(5 * 8));
-    codec.check(onc_frame_stream(codec.get(), dw, wire_len, doff, max_records, dres), "onc_frame_stream");
+    detail::Carve c{codec.stage(need<uint8_t>(wire_len) + need<uint64_t>(max_records + 1) + need<uint64_t>(5) +
+                                out_bytes(max_records))};
+    const auto w = c.take<uint8_t>(wire_len);
+    const auto off = c.take<uint64_t>(max_records + 1);
+    const auto res = c.take<uint64_t>(5);
+    if (wire_len) std::memcpy(w.host, wire, wire_len);
+    codec.check(onc_frame_stream(codec.get(), w.dev, wire_len, off.dev, max_records, res.dev), "onc_frame_stream");
     codec.sync();
     uint64_t r[5];
-    hip_check(hipMemcpy(r, dres, sizeof(r), hipMemcpyDeviceToHost), "D2H");
+    std::memcpy(r, res.host, sizeof(r));
     if (consumed) *consumed = size_t(r[1]);
     if (stop) {
         if (int32_t(r[2]) == ONC_OK) *stop = std::nullopt;
         else *stop = Error(int32_t(r[2]), uint32_t(r[3]), uint32_t(r[4]));
     }
-    return decode_device(codec, wire, dw, size_t(r[0]), doff, mode);
+    const size_t n = size_t(r[0]);
+    if (!n) return {};
+    const Out o = take_out(c, n);
+    const onc_decoded d = o.dev();
+    codec.check(onc_decode(codec.get(), w.dev, off.dev, n, int(mode), &d), "onc_decode");
+    codec.sync();
+    return results(o, n, wire);
 }
 
 // ----------------------------------------------------------------------------
@@ -1039,31 +1112,27 @@ struct BodyView {
 };
 
 inline BodyView decode_root(Codec& codec, int root, Bytes buf, DecodeMode mode, uint32_t param) {
-    DevBuf dw, doff, dp, dm, du, ds, d0, d1;
-    uint8_t* w = static_cast<uint8_t*>(dw.ensure(buf.len + 16));
-    if (buf.len) hip_check(hipMemcpy(w, buf.ptr, buf.len, hipMemcpyHostToDevice), "H2D");
-    const uint64_t off[2] = {0, buf.len};
-    uint64_t* o = static_cast<uint64_t*>(doff.ensure(sizeof(off)));
-    hip_check(hipMemcpy(o, off, sizeof(off), hipMemcpyHostToDevice), "H2D");
-    uint32_t* p = static_cast<uint32_t*>(dp.ensure(4));
-    hip_check(hipMemcpy(p, &param, 4, hipMemcpyHostToDevice), "H2D");
-    onc_decoded out{};
-    out.msgs = static_cast<onc_msg*>(dm.ensure(sizeof(onc_msg)));
-    out.unix_params = static_cast<onc_unix_params*>(du.ensure(2 * sizeof(onc_unix_params)));
-    out.status = static_cast<int32_t*>(ds.ensure(4));
-    out.aux0 = static_cast<uint32_t*>(d0.ensure(4));
-    out.aux1 = static_cast<uint32_t*>(d1.ensure(4));
-    codec.check(onc_decode_body(codec.get(), root, w, o, 1, int(mode), p, &out, nullptr), "onc_decode_body");
+    Carve c{codec.stage(need<uint8_t>(buf.len) + need<uint64_t>(2) + need<uint32_t>(1) + need<onc_msg>(1) +
+                        need<onc_unix_params>(2) + 3 * need<uint32_t>(1))};
+    const auto w = c.take<uint8_t>(buf.len);
+    const auto o = c.take<uint64_t>(2);
+    const auto p = c.take<uint32_t>(1);
+    const auto m = c.take<onc_msg>(1);
+    const auto u = c.take<onc_unix_params>(2);
+    const auto s = c.take<int32_t>(1);
+    const auto a0 = c.take<uint32_t>(1);
+    const auto a1 = c.take<uint32_t>(1);
+    if (buf.len) std::memcpy(w.host, buf.ptr, buf.len);
+    o.host[0] = 0;
+    o.host[1] = buf.len;
+    p.host[0] = param;
+    onc_decoded out{m.dev, u.dev, s.dev, a0.dev, a1.dev};
+    codec.check(onc_decode_body(codec.get(), root, w.dev, o.dev, 1, int(mode), p.dev, &out, nullptr), "onc_decode_body");
     codec.sync();
+    if (s.host[0] != ONC_OK) throw Error(s.host[0], a0.host[0], a1.host[0]);
     BodyView v;
-    int32_t st = 0;
-    uint32_t a0 = 0, a1 = 0;
-    hip_check(hipMemcpy(&v.d, out.msgs, sizeof(onc_msg), hipMemcpyDeviceToHost), "D2H");
-    hip_check(hipMemcpy(v.unix, out.unix_params, sizeof(v.unix), hipMemcpyDeviceToHost), "D2H");
-    hip_check(hipMemcpy(&st, out.status, 4, hipMemcpyDeviceToHost), "D2H");
-    hip_check(hipMemcpy(&a0, out.aux0, 4, hipMemcpyDeviceToHost), "D2H");
-    hip_check(hipMemcpy(&a1, out.aux1, 4, hipMemcpyDeviceToHost), "D2H");
-    if (st != ONC_OK) throw Error(st, a0, a1);
+    v.d = m.host[0];
+    std::memcpy(v.unix, u.host, sizeof(v.unix));
     return v;
 }
 
