@@ -450,14 +450,15 @@ def pcie_pipelined(args, torch, R, wl, hb, db, out, total_bytes, lens_np, rec_le
                     "copy; decoded AUTH_UNIX slots copied back for chunks with AUTH_UNIX auths" % K}
 
 
-def _event_ms(torch, fn, reps, dist, dev, sync_streams=()):
+def _event_ms(torch, fn, reps, sync_streams=()):
     """Average ms of `fn` over `reps` calls after one untimed call, by events
     on the current stream (every stream in sync_streams joined back into it
-    before the stop event), MAX over ranks."""
+    before the stop event). Local to the rank: the legs that use it reduce
+    their results over ranks afterwards (reduce_leg), outside any try block,
+    so a rank that fails a leg cannot leave the others waiting in a
+    collective."""
     fn()
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     cur = torch.cuda.current_stream()
@@ -470,11 +471,53 @@ def _event_ms(torch, fn, reps, dist, dev, sync_streams=()):
         cur.wait_stream(s)
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
-    t = torch.tensor([ms], dtype=torch.float64, device=cdev(dev))
+    return e0.elapsed_time(e1) / reps
+
+
+def _path(d, key):
+    for k in key.split(".") if key else []:
+        d = d.get(k) if isinstance(d, dict) else None
+    return d
+
+
+def reduce_leg(torch, dist, dev, res, keys, n_total):
+    """MAX over ranks of each sub-leg's ms_per_step (keys: dotted paths into
+    `res`, "" = res itself), AND of their `validated`; values recomputed
+    from the reduced times. Every rank calls it with the same keys, whatever
+    its legs did (a missing or failed sub-leg counts as +inf ms, not
+    validated)."""
+    import math
+    vals = []
+    for k in keys:
+        d = _path(res, k)
+        ms = d.get("ms_per_step") if isinstance(d, dict) else None
+        ok = bool(d.get("validated")) if isinstance(d, dict) else False
+        vals += [ms if (ms is not None and math.isfinite(ms)) else math.inf, 0.0 if ok else 1.0]
     if dist is not None:
+        t = torch.tensor(vals, dtype=torch.float64, device=cdev(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t[0])
+        vals = [float(x) for x in t.cpu()]
+    for i, k in enumerate(keys):
+        d = _path(res, k)
+        if not isinstance(d, dict):
+            continue
+        ms, bad = vals[2 * i], vals[2 * i + 1]
+        d["ms_per_step"] = ms if math.isfinite(ms) else None
+        d["value"] = n_total / (ms / 1e3) / 1e6 if math.isfinite(ms) else None
+        d["validated"] = bad == 0.0 and math.isfinite(ms)
+    return res
+
+
+def _pick_best(res, names):
+    """res.value / ms_per_step / best from the fastest validated sub-leg."""
+    cands = [k for k in names if isinstance(res.get(k), dict) and res[k].get("validated")]
+    if cands:
+        best = max(cands, key=lambda k: res[k]["value"])
+        res.update({"value": res[best]["value"], "ms_per_step": res[best]["ms_per_step"], "best": best})
+    else:
+        res.update({"value": None, "ms_per_step": None, "best": None})
+    res["validated"] = all(isinstance(res.get(k), dict) and res[k].get("validated") for k in names)
+    return res
 
 
 class MappedDecodeOut:
@@ -501,7 +544,7 @@ class MappedDecodeOut:
             b.close()
 
 
-def pcie_zero_copy(args, torch, R, wl, hb, codec, out, total_bytes, lens_np, rec_off, dec_off, dec, mode, dist,
+def pcie_zero_copy(args, torch, R, wl, hb, codec, out, total_bytes, lens_np, rec_off, dec_off, dec, mode,
                    n_total, has_unix):
     """PCIe-inclusive rate with nothing staged (ABI 7 onc_host_register): the
     bytes stay in mapped host memory and the kernels read and write them in
@@ -544,7 +587,7 @@ def pcie_zero_copy(args, torch, R, wl, hb, codec, out, total_bytes, lens_np, rec
 
             def step():
                 codec.decode_lengths(w, rl, n, 0, mode, o.msgs, o.unix, o.status, o.aux0, o.aux1, rec_off=o.off)
-            ms = _event_ms(torch, step, reps, dist, dev)
+            ms = _event_ms(torch, step, reps)
             ok = check_dec()
             rd = int(parsed_lines_bytes(lens_np))
             res.update({"value": n_total / (ms / 1e3) / 1e6, "ms_per_step": ms, "validated": ok,
@@ -567,7 +610,7 @@ def pcie_zero_copy(args, torch, R, wl, hb, codec, out, total_bytes, lens_np, rec
         def step_a():
             codec.encode(mb, wh, roh, sth, out_cap=total_bytes)
             codec.decode(wh, roh, n, mode, o.msgs, o.unix, o.status, o.aux0, o.aux1)
-        ms_a = _event_ms(torch, step_a, reps, dist, dev)
+        ms_a = _event_ms(torch, step_a, reps)
         ok_a = check_dec(with_off=False) and bool((sth.view(np.int32)[:n] == 0).all())
         ok_a = ok_a and np.array_equal(roh.view(np.int64)[:n + 1], ref_off)
         ref_wire = out[:total_bytes].cpu().numpy()
@@ -589,7 +632,7 @@ def pcie_zero_copy(args, torch, R, wl, hb, codec, out, total_bytes, lens_np, rec
                 h_off.copy_(rec_off[:n + 1], non_blocking=True)
                 h_st.copy_(st, non_blocking=True)
             codec.decode(out, rec_off, n, mode, o.msgs, o.unix, o.status, o.aux0, o.aux1)
-        ms_b = _event_ms(torch, step_b, reps, dist, dev, sync_streams=(cs,))
+        ms_b = _event_ms(torch, step_b, reps, sync_streams=(cs,))
         torch.cuda.synchronize()
         ok_b = check_dec(with_off=False) and bool((h_st[:n] == 0).all())
         ok_b = ok_b and np.array_equal(h_off.numpy(), ref_off) and np.array_equal(h_wire.numpy(), ref_wire)
@@ -604,9 +647,7 @@ def pcie_zero_copy(args, torch, R, wl, hb, codec, out, total_bytes, lens_np, rec
                                   "note": "encode reads descriptors + arenas in place into an HBM wire; the wire, "
                                           "offsets and statuses come back on a copy stream while the decode "
                                           "writes its outputs into mapped host memory"}}
-        best = max(var, key=lambda k: var[k]["value"] if var[k]["validated"] else -1)
-        res.update({"value": var[best]["value"], "ms_per_step": var[best]["ms_per_step"], "best": best,
-                    "validated": ok_a and ok_b, "variants": var})
+        res["variants"] = var                         # best picked after the reduction over ranks
         return res
     except Exception as e:                            # report, do not lose the line
         res.update({"value": None, "validated": False, "error": repr(e)})
@@ -649,7 +690,7 @@ def iov_gather_ok(hdr, e, payload, ref_wire, wire_base=0, step=1 << 16):
     return True
 
 
-def pcie_iov(args, torch, R, L, hb, db, codec, n_total, hdr_total, total_bytes, out, dist):
+def pcie_iov(args, torch, R, L, hb, db, codec, n_total, hdr_total, total_bytes, out):
     """PCIe-inclusive legs of the vectored encode (onc_encode_iov): the
     payloads never cross the link (README.md:71-75, rpc_message.rs:19 — the
     sender's writev gathers them from where they lie); the payload arena
@@ -699,7 +740,7 @@ def pcie_iov(args, torch, R, L, hb, db, codec, n_total, hdr_total, total_bytes, 
             hdr_h.copy_(hdr_d[:hdr_total], non_blocking=True)
             iov_h.copy_(iov_d[:32 * n], non_blocking=True)
             st_h.copy_(st_d[:n], non_blocking=True)
-        ms = _event_ms(torch, ser, reps, dist, dev)
+        ms = _event_ms(torch, ser, reps)
         ok = bool((st_h == 0).all()) and iov_gather_ok(hdr_h.numpy(), iov_h.numpy().view(L.IOV_DTYPE), pay, ref_wire)
         res["serialised"] = {"value": n_total / (ms / 1e3) / 1e6, "ms_per_step": ms, "validated": ok,
                              "h2d_bytes_per_gpu": h2d, "d2h_bytes_per_gpu": d2h,
@@ -743,7 +784,7 @@ def pcie_iov(args, torch, R, L, hb, db, codec, n_total, hdr_total, total_bytes, 
                 s_out.wait_stream(s_k)
                 with torch.cuda.stream(s_out):
                     slab_h.copy_(slab, non_blocking=True)
-        ms_p = _event_ms(torch, pipe, reps, dist, dev, sync_streams=(s_in, s_k, s_out))
+        ms_p = _event_ms(torch, pipe, reps, sync_streams=(s_in, s_k, s_out))
         okp = True
         for cp, sub, slab, slab_h, hb_k, o_hdr, o_iov, nk, lo in plans:
             sh = slab_h.numpy()
@@ -766,18 +807,14 @@ def pcie_iov(args, torch, R, L, hb, db, codec, n_total, hdr_total, total_bytes, 
 
         def zc():
             codec.encode_iov(mb, hdr_m, iov_m, st_m, None, hdr_total)
-        ms_z = _event_ms(torch, zc, reps, dist, dev)
+        ms_z = _event_ms(torch, zc, reps)
         okz = bool((st_m.view(np.int32)[:n] == 0).all()) and iov_gather_ok(
             hdr_m.host[:hdr_total], iov_m.view(L.IOV_DTYPE)[:n], pay, ref_wire)
         res["zero_copy"] = {"value": n_total / (ms_z / 1e3) / 1e6, "ms_per_step": ms_z, "validated": okz,
                             "h2d_bytes_per_gpu": h2d, "d2h_bytes_per_gpu": d2h,
                             "note": "onc_host_register: iov_len / iov_emit read the descriptors and write the "
                                     "headers, iovecs and statuses in host memory in place"}
-        best = max(("serialised", "pipelined", "zero_copy"),
-                   key=lambda k: res[k]["value"] if res[k]["validated"] else -1)
-        res.update({"value": res[best]["value"], "ms_per_step": res[best]["ms_per_step"], "best": best,
-                    "validated": ok and okp and okz})
-        return res
+        return res                                    # best picked after the reduction over ranks
     except Exception as e:
         res.update({"value": None, "validated": False, "error": repr(e)})
         return res
@@ -1369,11 +1406,24 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
         pcie["pipelined"] = pcie_pipelined(args, torch, R, wl, hb, db, out, total_bytes, lens_np, rec_len,
                                            dec_off, dec, mode, h_in, local_rank, dist, n_total)
         kinds = np.concatenate([hb.msgs["cred_kind_len"] >> 24, hb.msgs["verf_kind_len"] >> 24])
-        pcie["zero_copy"] = pcie_zero_copy(args, torch, R, wl, hb, codec, out, total_bytes, lens_np, rec_off,
-                                           dec_off, dec, mode, dist, n_total,
-                                           bool((kinds == L.KIND_UNIX).any()))
+        barrier()
+        zc = pcie_zero_copy(args, torch, R, wl, hb, codec, out, total_bytes, lens_np, rec_off, dec_off, dec, mode,
+                            n_total, bool((kinds == L.KIND_UNIX).any()))
+        if wl == "c2":
+            zc = reduce_leg(torch, dist, dev, zc, [""], n_total)
+        else:
+            zc.setdefault("variants", {})
+            zc = reduce_leg(torch, dist, dev, zc, ["variants.in_place", "variants.wire_on_device"], n_total)
+            _pick_best(zc["variants"], ["in_place", "wire_on_device"])
+            v = zc["variants"]
+            zc.update({"value": v.pop("value"), "ms_per_step": v.pop("ms_per_step"), "best": v.pop("best"),
+                       "validated": v.pop("validated")})
+        pcie["zero_copy"] = zc
     elif args.iov and not args.no_pcie:
-        pcie = pcie_iov(args, torch, R, L, hb, db, codec, n_total, iov_hdr_total, total_bytes, out, dist)
+        barrier()
+        pcie = pcie_iov(args, torch, R, L, hb, db, codec, n_total, iov_hdr_total, total_bytes, out)
+        pcie = reduce_leg(torch, dist, dev, pcie, ["serialised", "pipelined", "zero_copy"], n_total)
+        _pick_best(pcie, ["serialised", "pipelined", "zero_copy"])
 
     steps = args.steps
     ms_per_step = ms_max / steps

@@ -125,3 +125,20 @@ def test_parsed_lines_bytes():
     starts = np.arange(8) * 300
     want = sum(((s + 47) // 128 - s // 128 + 1) * 128 for s in starts)
     assert bm.parsed_lines_bytes(lens) == want
+
+
+def test_reduce_leg_and_best():
+    """bench.reduce_leg (the over-ranks reduction of the PCIe-inclusive legs,
+    here on one rank): values recomputed from ms, a failed or missing
+    sub-leg is unvalidated with no value; _pick_best takes the fastest
+    validated one."""
+    import torch
+    bm = _bench()
+    res = {"serialised": {"ms_per_step": 2.0, "validated": True},
+           "pipelined": {"ms_per_step": 4.0, "validated": True},
+           "zero_copy": {"error": "x"}}
+    res = bm.reduce_leg(torch, None, "cpu", res, ["serialised", "pipelined", "zero_copy", "missing"], 1_000_000)
+    assert res["serialised"]["value"] == 500.0 and res["pipelined"]["value"] == 250.0
+    assert res["zero_copy"]["value"] is None and not res["zero_copy"]["validated"]
+    bm._pick_best(res, ["serialised", "pipelined", "zero_copy"])
+    assert res["best"] == "serialised" and res["value"] == 500.0 and not res["validated"]
