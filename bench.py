@@ -585,16 +585,32 @@ def pcie_zero_copy(args, torch, R, wl, hb, codec, out, total_bytes, lens_np, rec
             rl = R.HostMapped.from_array(codec, lens_np.astype(np.uint32))
             keep.append(rl)
 
-            def step():
-                codec.decode_lengths(w, rl, n, 0, mode, o.msgs, o.unix, o.status, o.aux0, o.aux1, rec_off=o.off)
+            if args.frame:
+                # the raw socket buffer: framed on the device where it lies
+                # (onc_frame_stream, rpc_message.rs:343-367), then decoded in place
+                fres = torch.zeros(5, dtype=torch.int64, device=dev)
+
+                def step():
+                    codec.frame_stream(w, total_bytes, o.off, n, fres)
+                    codec.decode(w, o.off, n, mode, o.msgs, o.unix, o.status, o.aux0, o.aux1)
+            else:
+                def step():
+                    codec.decode_lengths(w, rl, n, 0, mode, o.msgs, o.unix, o.status, o.aux0, o.aux1,
+                                         rec_off=o.off)
             ms = _event_ms(torch, step, reps)
             ok = check_dec()
+            if args.frame:
+                ok = ok and [int(x) for x in fres.cpu()[:3]] == [n, total_bytes, 0]
             rd = int(parsed_lines_bytes(lens_np))
             res.update({"value": n_total / (ms / 1e3) / 1e6, "ms_per_step": ms, "validated": ok,
-                        "h2d_bytes_touched_per_gpu": rd + 4 * n, "d2h_bytes_per_gpu": o.nbytes(n, has_unix),
+                        "h2d_bytes_touched_per_gpu": rd + (0 if args.frame else 4 * n),
+                        "d2h_bytes_per_gpu": o.nbytes(n, has_unix),
                         "h2d_note": "the 128-byte lines holding each record's first 48 bytes (the decode's "
-                                    "first window round; longer headers read more) + 4 B of length per record; "
-                                    f"the wire is {total_bytes} bytes"})
+                                    "first window round; longer headers read more)" +
+                                    (" + the framer's sweep and chase reads" if args.frame else
+                                     " + 4 B of length per record") + f"; the wire is {total_bytes} bytes",
+                        "step": ("onc_frame_stream + onc_decode of the mapped socket buffer" if args.frame else
+                                 "onc_decode_lengths of the mapped socket buffer from its mapped lengths")})
             return res
         # loopbacks
         mb = R.MappedHostBatch(codec, hb)

@@ -649,6 +649,36 @@ struct Decoded {
 };
 
 // ----------------------------------------------------------------------------
+// HostRegistration: a caller's receive buffer mapped for the kernels
+// (onc_host_register, ABI 7). BatchDecoder given one decodes the bytes where
+// they lie — no copy into the stage; only the 16-byte granules of the headers
+// it parses cross PCIe (call_body.rs:53-59: payloads are slices, never read).
+// Registration pins the pages (a server maps its socket buffers once);
+// unpinned on destruction, so it must outlive the decodes using it.
+// ----------------------------------------------------------------------------
+class HostRegistration {
+public:
+    HostRegistration(Codec& codec, const uint8_t* buf, size_t len) : codec_(codec), host_(buf), len_(len) {
+        void* d = nullptr;
+        codec.check(onc_host_register(codec.get(), const_cast<uint8_t*>(buf), len ? len : 1, &d),
+                    "onc_host_register");
+        dev_ = static_cast<const uint8_t*>(d);
+    }
+    ~HostRegistration() { (void)onc_host_unregister(codec_.get(), const_cast<uint8_t*>(host_)); }
+    HostRegistration(const HostRegistration&) = delete;
+    HostRegistration& operator=(const HostRegistration&) = delete;
+    const uint8_t* host() const { return host_; }
+    const uint8_t* dev() const { return dev_; }
+    size_t size() const { return len_; }
+
+private:
+    Codec& codec_;
+    const uint8_t* host_;
+    const uint8_t* dev_ = nullptr;
+    size_t len_;
+};
+
+// ----------------------------------------------------------------------------
 // BatchDecoder: try_from of many records (one buffer per record)
 // ----------------------------------------------------------------------------
 class BatchDecoder {
@@ -669,7 +699,24 @@ public:
                                          DecodeMode mode = DecodeMode::Slice, size_t* consumed = nullptr,
                                          std::optional<Error>* stop = nullptr);
 
+    // The same over a registered (mapped) buffer, decoded in place.
+    std::vector<Decoded> try_from(Codec& codec, const HostRegistration& wire, const std::vector<uint32_t>& rec_len,
+                                  DecodeMode mode = DecodeMode::Slice) {
+        return lengths_at(codec, wire.host(), wire.dev(), wire.size(), rec_len, mode);
+    }
+    std::vector<Decoded> try_from_stream(Codec& codec, const HostRegistration& wire,
+                                         DecodeMode mode = DecodeMode::Slice, size_t* consumed = nullptr,
+                                         std::optional<Error>* stop = nullptr) {
+        return stream_at(codec, wire.host(), wire.dev(), wire.size(), mode, consumed, stop);
+    }
+
 private:
+    // dev_wire: the kernels' address of `wire` (a registration), or null:
+    // the wire is copied into the stage first
+    std::vector<Decoded> lengths_at(Codec& codec, const uint8_t* wire, const uint8_t* dev_wire, size_t wire_len,
+                                    const std::vector<uint32_t>& rec_len, DecodeMode mode);
+    std::vector<Decoded> stream_at(Codec& codec, const uint8_t* wire, const uint8_t* dev_wire, size_t wire_len,
+                                   DecodeMode mode, size_t* consumed, std::optional<Error>* stop);
     // the decode outputs in staging regions, read after the synchronisation
     struct Out {
         detail::Region<onc_msg> msgs;
@@ -1023,17 +1070,27 @@ inline std::vector<Decoded> BatchDecoder::results(const Out& o, size_t n, const 
 // one pass); the outputs land in the stage.
 inline std::vector<Decoded> BatchDecoder::try_from(Codec& codec, const uint8_t* wire, size_t wire_len,
                                                    const std::vector<uint32_t>& rec_len, DecodeMode mode) {
+    return lengths_at(codec, wire, nullptr, wire_len, rec_len, mode);
+}
+
+inline std::vector<Decoded> BatchDecoder::lengths_at(Codec& codec, const uint8_t* wire, const uint8_t* dev_wire,
+                                                     size_t wire_len, const std::vector<uint32_t>& rec_len,
+                                                     DecodeMode mode) {
     using detail::need;
     const size_t n = rec_len.size();
     if (!n) return {};
-    detail::Carve c{codec.stage(need<uint8_t>(wire_len) + need<uint32_t>(n) + out_bytes(n))};
-    const auto w = c.take<uint8_t>(wire_len);
+    detail::Carve c{codec.stage((dev_wire ? 0 : need<uint8_t>(wire_len)) + need<uint32_t>(n) + out_bytes(n))};
+    const uint8_t* wd = dev_wire;
+    if (!dev_wire) {
+        const auto w = c.take<uint8_t>(wire_len);
+        if (wire_len) std::memcpy(w.host, wire, wire_len);
+        wd = w.dev;
+    }
     const auto l = c.take<uint32_t>(n);
-    if (wire_len) std::memcpy(w.host, wire, wire_len);
     std::memcpy(l.host, rec_len.data(), n * 4);
     const Out o = take_out(c, n);
     const onc_decoded d = o.dev();
-    codec.check(onc_decode_lengths(codec.get(), w.dev, l.dev, n, 0, int(mode), nullptr, &d), "onc_decode_lengths");
+    codec.check(onc_decode_lengths(codec.get(), wd, l.dev, n, 0, int(mode), nullptr, &d), "onc_decode_lengths");
     codec.sync();
     return results(o, n, wire);
 }
@@ -1041,15 +1098,25 @@ inline std::vector<Decoded> BatchDecoder::try_from(Codec& codec, const uint8_t* 
 inline std::vector<Decoded> BatchDecoder::try_from_stream(Codec& codec, const uint8_t* wire, size_t wire_len,
                                                           DecodeMode mode, size_t* consumed,
                                                           std::optional<Error>* stop) {
+    return stream_at(codec, wire, nullptr, wire_len, mode, consumed, stop);
+}
+
+inline std::vector<Decoded> BatchDecoder::stream_at(Codec& codec, const uint8_t* wire, const uint8_t* dev_wire,
+                                                    size_t wire_len, DecodeMode mode, size_t* consumed,
+                                                    std::optional<Error>* stop) {
     using detail::need;
     const size_t max_records = wire_len / 4 + 1;   // every record is at least 4 bytes
-    detail::Carve c{codec.stage(need<uint8_t>(wire_len) + need<uint64_t>(max_records + 1) + need<uint64_t>(5) +
-                                out_bytes(max_records))};
-    const auto w = c.take<uint8_t>(wire_len);
+    detail::Carve c{codec.stage((dev_wire ? 0 : need<uint8_t>(wire_len)) + need<uint64_t>(max_records + 1) +
+                                need<uint64_t>(5) + out_bytes(max_records))};
+    const uint8_t* wd = dev_wire;
+    if (!dev_wire) {
+        const auto w = c.take<uint8_t>(wire_len);
+        if (wire_len) std::memcpy(w.host, wire, wire_len);
+        wd = w.dev;
+    }
     const auto off = c.take<uint64_t>(max_records + 1);
     const auto res = c.take<uint64_t>(5);
-    if (wire_len) std::memcpy(w.host, wire, wire_len);
-    codec.check(onc_frame_stream(codec.get(), w.dev, wire_len, off.dev, max_records, res.dev), "onc_frame_stream");
+    codec.check(onc_frame_stream(codec.get(), wd, wire_len, off.dev, max_records, res.dev), "onc_frame_stream");
     codec.sync();
     uint64_t r[5];
     std::memcpy(r, res.host, sizeof(r));
@@ -1062,7 +1129,7 @@ inline std::vector<Decoded> BatchDecoder::try_from_stream(Codec& codec, const ui
     if (!n) return {};
     const Out o = take_out(c, n);
     const onc_decoded d = o.dev();
-    codec.check(onc_decode(codec.get(), w.dev, off.dev, n, int(mode), &d), "onc_decode");
+    codec.check(onc_decode(codec.get(), wd, off.dev, n, int(mode), &d), "onc_decode");
     codec.sync();
     return results(o, n, wire);
 }

@@ -343,6 +343,21 @@ static void test_batch_round_trip(Codec& c) {
             CHECK(*out[i].message == msgs[i]);
         }
     }
+    // the same send buffer registered (onc_host_register) and decoded where it lies
+    const HostRegistration reg(c, wire.data(), wire.size());
+    for (DecodeMode mode : {DecodeMode::Slice, DecodeMode::Bytes}) {
+        const std::vector<Decoded> out = dec.try_from(c, reg, rec_len, mode);
+        CHECK(out.size() == msgs.size());
+        for (size_t i = 0; i < msgs.size(); ++i) {
+            CHECK(out[i].ok());
+            CHECK(*out[i].message == msgs[i]);
+        }
+    }
+    size_t consumed = 0;
+    std::optional<Error> stop;
+    const std::vector<Decoded> framed = dec.try_from_stream(c, reg, DecodeMode::Slice, &consumed, &stop);
+    CHECK(framed.size() == msgs.size() && consumed == wire.size() && !stop.has_value());
+    for (size_t i = 0; i < msgs.size(); ++i) CHECK(framed[i].ok() && *framed[i].message == msgs[i]);
 }
 
 // The caller's loop over a socket buffer (expected_message_len + one-message
