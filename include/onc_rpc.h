@@ -374,6 +374,9 @@ typedef struct onc_codec onc_codec;
 #define ONC_VARIANT_EMIT_PRELOAD     0x80000u  /* wave-per-tile enc_emit: preload the AUTH_UNIX credential block (lab) */
 #define ONC_VARIANT_DEC_AUX_SPARSE   0x100000u /* decode: aux0/aux1 written only for failing records (lab;
                                                   the outputs of OK records' aux words are then undefined) */
+#define ONC_VARIANT_SINGLE_PASS      0x200000u /* onc_encode without the length pass: the wave-per-tile
+                                                  enc_emit claims tiles in start order and places them by a
+                                                  decoupled look-back (lab; one plan chunk, RpcMessage root) */
 
 #define ONC_OPT_FORCE_SCAN 0x1u   /* always launch the separate block-scan kernels (tests of that path) */
 

@@ -592,10 +592,38 @@ int enc_emit(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_ca
 // offset from rec_off[k's end], which chunk k's emit wrote.
 constexpr uint64_t kEncChunk = onc::kFusedBlocks * onc::kLenRecs;   // 1M records
 
+// ONC_VARIANT_SINGLE_PASS (lab): no enc_len launch — the wave-per-tile
+// enc_emit plans its tiles and places them by a decoupled look-back over
+// per-tile words in the scratch (encode.hip tile_lookback), zeroed by one
+// fill before the launch: the states of the tiles, then the claim counter
+// and the give-up flag.
+int single_pass(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
+                int32_t* status, uint32_t* rec_len) {
+    onc::EncArgs a;
+    int rc = enc_args(c, batch, status, rec_len, a);
+    if (rc != ONC_RC_OK) return rc;
+    forget_plan(c);
+    a.ws = 0;
+    a.block_pay = nullptr;
+    a.origin = reinterpret_cast<uintptr_t>(out) & 15;
+    a.out = out - a.origin;
+    a.out_cap = out ? a.origin + out_cap : 0;
+    a.rec_off = rec_off;
+    a.rec_len = rec_len;
+    const uint64_t ntiles = onc::num_emit_tiles(batch->n);
+    a.lb_state = c->scratch;                                   // ntiles + 1 words (< 3T)
+    a.lb_fail = reinterpret_cast<uint32_t*>(c->scratch + ntiles) + 1;
+    const hipError_t e = hipMemsetAsync(a.lb_state, 0, (ntiles + 1) * sizeof(uint64_t), c->stream);
+    if (e != hipSuccess) return fail(c, e, "hipMemsetAsync");
+    return run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
+}
+
 int encode_batch(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
                  int32_t* status, uint32_t* rec_len, uint32_t root) {
     const uint64_t n = batch->n;
     const uint64_t chunk = c->enc_chunk ? c->enc_chunk : kEncChunk;
+    if ((c->variant & ONC_VARIANT_SINGLE_PASS) && root == ONC_ROOT_RPC_MESSAGE && n <= chunk)
+        return single_pass(c, batch, out, out_cap, rec_off, status, rec_len);
     if (n <= chunk || (c->variant & ONC_VARIANT_WHOLE_PLAN)) {     // whole-batch plan (lab)
         const int rc = enc_plan(c, batch, status, rec_len, root);
         if (rc != ONC_RC_OK) return rc;

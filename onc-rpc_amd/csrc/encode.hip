@@ -581,8 +581,63 @@ __device__ __forceinline__ void img_placeholder(uint32_t* img32, ImgSink& w, uin
     w.prev = 0u;
 }
 
+// Single pass (ONC_VARIANT_SINGLE_PASS, lab): the tile's place without an
+// enc_len launch. Tiles are claimed in start order (enc_emit_kernel_t), so a
+// wave only ever waits on tiles claimed earlier by waves that are running or
+// done — no deadlock when the grid is not fully resident. The wave publishes
+// its tile's total, sums the totals of its predecessors from the nearest one
+// that has published its inclusive prefix (256 states per round, one load
+// per lane per 64), and publishes its own prefix. A wave that finds a
+// predecessor not yet published re-reads; past kLbSpinLimit rounds it gives
+// up and flags lb_fail (a bound, never a hang).
+constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
+constexpr uint32_t kLbSpinLimit = 1u << 22;
+__device__ __forceinline__ uint64_t tile_lookback(const EncArgs& a, uint64_t t, uint64_t agg) {
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) __hip_atomic_store(a.lb_state + t, kLbAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t excl = 0;
+    int64_t j = int64_t(t);                        // tiles [0, j) not summed yet
+    uint32_t spins = 0;
+    while (j > 0) {
+        uint64_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t idx = j - 1 - lane - 64 * k;
+            v[k] = idx >= 0 ? __hip_atomic_load(a.lb_state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+        }
+        bool done = false, retry = false;
+        uint64_t sum = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (done || retry) continue;
+            const uint64_t incl = __ballot((v[k] >> 62) == 2);
+            const uint64_t empty = __ballot((v[k] >> 62) == 0);
+            const int first = incl ? __builtin_ctzll(incl) : 64;
+            const uint64_t upto = first == 64 ? ~0ull : ((2ull << first) - 1);     // lanes <= first
+            if (empty & upto) {
+                retry = true;
+            } else {
+                sum += lane_u64(wave_incl_scan_u64(uint64_t(lane) <= uint64_t(first) ? (v[k] & kLbVal) : 0), 63);
+                done = first < 64;
+            }
+        }
+        if (retry) {
+            if (++spins > kLbSpinLimit) {
+                if (lane == 0) atomicOr(a.lb_fail, 1u);
+                break;
+            }
+            continue;                               // this round's sums dropped: read it again
+        }
+        excl += sum;
+        if (done) break;
+        j -= 256;
+    }
+    if (lane == 0) __hip_atomic_store(a.lb_state + t, kLbIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
 template <int kU, int kNT, bool kFused, bool kRoot = false, bool kGiven = false, bool kPre = false,
-          bool kLen = false>
+          bool kLen = false, bool kSingle = false>
 __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile, uint64_t given = 0) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = tile * kEmitRecs;
@@ -593,12 +648,15 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     // Prologue: the tile-placement loads and this lane's descriptor issued
     // together, one memory round trip before the planning starts.
     ONC_PROF(0);
-    TileLoads<kFused> tl = tile_loads<kFused, kGiven>(a, tile, given);
+    TileLoads<kFused> tl;
+    if constexpr (!kSingle) tl = tile_loads<kFused, kGiven>(a, tile, given);
     MsgRegs mr = issue_msg(a.msgs + r0 + min(lane, nrec - 1));
     // kLen: the plan's length of the lane's record, issued with the rest
     uint32_t glen = 0;
     if constexpr (kLen) glen = a.len_in[r0 + min(lane, nrec - 1)];
-    if constexpr (kFused) {
+    if constexpr (kSingle) {
+        asm volatile("" : "+v"(mr.q[0]), "+v"(mr.q[1]), "+v"(mr.q[2]), "+v"(mr.q[3]));
+    } else if constexpr (kFused) {
         static_assert(TileLoads<kFused>::kW == 16, "pin list below");
         asm volatile("" : "+v"(mr.q[0]), "+v"(mr.q[1]), "+v"(mr.q[2]), "+v"(mr.q[3]), "+v"(tl.v),
                      "+v"(tl.w[0]), "+v"(tl.w[1]), "+v"(tl.w[2]), "+v"(tl.w[3]), "+v"(tl.w[4]), "+v"(tl.w[5]),
@@ -611,7 +669,8 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     const onc_msg dm = as_msg(mr);
     // output coordinates: byte 0 = the 16-aligned chunk base below the
     // caller's `out`, which sits at `origin` (any writer position)
-    const uint64_t T0 = a.origin + (kGiven ? 0ull : launch_base(a)) + tile_reduce<kFused>(tl, tile);
+    uint64_t T0 = 0;
+    if constexpr (!kSingle) T0 = a.origin + (kGiven ? 0ull : launch_base(a)) + tile_reduce<kFused>(tl, tile);
     ONC_PROF(1);
     uint64_t len = 0, poff = 0;
     uint32_t hw = 0;
@@ -633,6 +692,14 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                               (d.msg_type == ONC_MSG_REPLY && d.reply_stat == ONC_REPLY_ACCEPTED &&
                                d.stat == ONC_ACCEPT_SUCCESS);
             hw = len ? uint32_t((len - (body ? uint64_t(d.payload_len) : 0ull)) >> 2) : 0;
+        } else if constexpr (kSingle) {
+            // enc_len's plan of the record (its decl 1 form) and its outputs
+            RecPlan p = plan_record<true>(d, a.unix, a.bounds);
+            if (p.status != ONC_OK) p = plan_record<false>(d, a.unix, a.bounds);
+            a.status[r0 + lane] = p.status;
+            if (a.rec_len) a.rec_len[r0 + lane] = uint32_t(p.len);
+            len = p.len;
+            hw = len ? meta_hw(p.meta) : 0;
         } else {
             // the same function as enc_len: lengths agree (declared AUTH_UNIX
             // lengths: no parameter-block load here)
@@ -644,6 +711,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((payload + d.payload_off) & 3) == 0);
     }
     const uint64_t incl = wave_incl_scan_u64(len);
+    if constexpr (kSingle) T0 = a.origin + launch_base(a) + tile_lookback(a, tile, lane_u64(incl, 63));
     const uint64_t start = T0 + incl - len;
     const uint64_t en = start + len;
     const uint64_t pst = start + 4ull * hw;
@@ -1247,12 +1315,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
 // kernel boundary). The message instances need 106 VGPRs (4 waves per SIMD;
 // held there by the attribute); squeezed to 5 waves per SIMD (96 VGPRs) they
 // spill. The body-root instances keep what they need (140 VGPRs).
-template <int kU, int kNT = 0, bool kFused = false, bool kRoot = false, bool kLen = false, bool kPre = false>
+template <int kU, int kNT = 0, bool kFused = false, bool kRoot = false, bool kLen = false, bool kPre = false,
+          bool kSingle = false>
 __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(kRoot ? 1 : 4))) void enc_emit_kernel_t(EncArgs a) {
     __shared__ ImgTile s_tiles[kFastWaves];
-    const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
+    uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
+    if constexpr (kSingle) {
+        // tiles claimed in start order (the claim counter is the word after the tiles' states)
+        uint32_t t = 0;
+        if ((threadIdx.x & 63) == 0) t = atomicAdd(reinterpret_cast<uint32_t*>(a.lb_state + num_emit_tiles(a.n)), 1u);
+        tile = uint32_t(__builtin_amdgcn_readfirstlane(int(t)));
+    }
     if (tile < num_emit_tiles(a.n))
-        enc_emit_tile<kU, kNT, kFused, kRoot, false, kPre, kLen>(a, s_tiles[threadIdx.x >> 6], tile);
+        enc_emit_tile<kU, kNT, kFused, kRoot, false, kPre, kLen, kSingle>(a, s_tiles[threadIdx.x >> 6], tile);
 }
 
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
@@ -1290,6 +1365,10 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     const dim3 g{uint32_t(blocks)}, b{uint32_t(64 * kFastWaves)};
+    if (a.lb_state) {                               // (lab: the single pass, codec.hip single_pass)
+        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false, false, false, false, true>), g, b, 0, s, a);
+        return hipGetLastError();
+    }
     if (a.variant & ONC_VARIANT_EMIT_PRELOAD) {     // (lab: the round-3 credential-block preload)
         if (a.len_in) {
             if (a.fused_base) ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, true, false, true, true>), g, b, 0, s, a);

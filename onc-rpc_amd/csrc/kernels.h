@@ -63,6 +63,12 @@ struct EncArgs {
     const uint64_t* base_dev;   // optional: output bytes before this launch's first record (chunked encode)
     const uint32_t* len_in;     // optional (wave-per-tile enc_emit): the plan's record lengths, read instead
                                 // of re-planning (no dependent AUTH_UNIX parameter load in the prologue)
+    // single pass (ONC_VARIANT_SINGLE_PASS, lab): no enc_len launch; every emit wave claims a tile id in
+    // start order, plans it and places it by a decoupled look-back over these words (zeroed before the
+    // launch): lb_state[tile] = flag << 62 | bytes (1: the tile's own total, 2: the inclusive prefix);
+    // lb_state[ntiles] = the claim counter
+    uint64_t* lb_state;
+    uint32_t* lb_fail;          // set when a look-back gave up (a bound on its spins: never a hang)
 #ifdef ONC_EMIT_PROF
     uint64_t* prof;         // lab builds only (tools/emit_prof.hip): per-tile phase timestamps
 #endif
@@ -76,7 +82,7 @@ constexpr uint64_t kFusedBlocks = 1024;
 struct IovArgs {
     uint64_t n;
     // (extents follow the declared AUTH_UNIX lengths as onc_encode places them; a record failing only a
-    // deferred block check takes its extent with no header bytes and a zero-length iovec)
+    // deferred block check takes its extent with the placeholder header, include/onc_rpc.h onc_auth)
     const onc_msg* msgs;
     const onc_unix_params* unix;
     const uint8_t* auth_arena;

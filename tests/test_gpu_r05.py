@@ -362,3 +362,27 @@ def test_c4_device_byte_check_across_chunks(R):
         c.close()
         del db
         torch.cuda.empty_cache()
+
+
+# ---------------------------------------------------------------------------
+# single pass (ONC_VARIANT_SINGLE_PASS, lab): no enc_len launch
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("kind", ["mixed", "unix16", "adversarial", "call_none"])
+def test_single_pass_encode_bit_exact(R, oracle, kind):
+    """The single-pass encode (tiles claimed in start order, placed by a
+    decoupled look-back inside the wave-per-tile enc_emit) produces the
+    oracle's bytes, offsets, statuses and lengths — at two writer positions
+    and with a capacity inside the batch — and its output decodes."""
+    from test_gpu_emit_paths import _enc_oracle_sized, _adversarial
+    hb = {"mixed": lambda: S.mixed(70_001, seed=91, pmin=0, pmax=900, exotic=0.2),
+          "unix16": lambda: S.call_unix16(50_000, 64, seed=92),
+          "adversarial": lambda: _adversarial(93, n=5000),
+          "call_none": lambda: S.call_none(300_000, 256, seed=94)}[kind]()
+    c = R.Codec(0, variant=R.VARIANT_SINGLE_PASS)
+    try:
+        o_st, o_len = _enc_oracle_sized(R, c, hb, oracle)
+        _enc_oracle_sized(R, c, hb, oracle, shift=5)
+        total = int(o_len.astype(np.int64).sum())
+        _enc_oracle_sized(R, c, hb, oracle, shift=3, cap=total // 3 + 7)
+    finally:
+        c.close()
