@@ -592,6 +592,10 @@ __device__ __forceinline__ void img_placeholder(uint32_t* img32, ImgSink& w, uin
 // up and flags lb_fail (a bound, never a hang).
 constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
 constexpr uint32_t kLbSpinLimit = 1u << 22;
+#ifndef ONC_LB_W
+#define ONC_LB_W 16
+#endif
+constexpr int kLbW = ONC_LB_W;                    // states per lane per round (64 * kLbW per round)
 __device__ __forceinline__ uint64_t tile_lookback(const EncArgs& a, uint64_t t, uint64_t agg) {
     const int lane = threadIdx.x & 63;
     if (lane == 0) __hip_atomic_store(a.lb_state + t, kLbAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -599,16 +603,16 @@ __device__ __forceinline__ uint64_t tile_lookback(const EncArgs& a, uint64_t t, 
     int64_t j = int64_t(t);                        // tiles [0, j) not summed yet
     uint32_t spins = 0;
     while (j > 0) {
-        uint64_t v[4];
+        uint64_t v[kLbW];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kLbW; ++k) {
             const int64_t idx = j - 1 - lane - 64 * k;
             v[k] = idx >= 0 ? __hip_atomic_load(a.lb_state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
         }
         bool done = false, retry = false;
         uint64_t sum = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kLbW; ++k) {
             if (done || retry) continue;
             const uint64_t incl = __ballot((v[k] >> 62) == 2);
             const uint64_t empty = __ballot((v[k] >> 62) == 0);
@@ -630,7 +634,7 @@ __device__ __forceinline__ uint64_t tile_lookback(const EncArgs& a, uint64_t t, 
         }
         excl += sum;
         if (done) break;
-        j -= 256;
+        j -= 64 * kLbW;
     }
     if (lane == 0) __hip_atomic_store(a.lb_state + t, kLbIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return excl;

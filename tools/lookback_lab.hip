@@ -107,6 +107,7 @@ __global__ __launch_bounds__(256) void lookback_kernel(const onc_msg* msgs, uint
 }
 
 int main(int argc, char** argv) {
+    setvbuf(stdout, nullptr, _IONBF, 0);
     const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 1000000;
     const uint64_t ntiles = (n + 63) / 64;
     std::vector<onc_msg> m(n);
@@ -130,17 +131,17 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1, e2;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&e2));
     struct Cfg { const char* name; uint32_t grid; int w; };
-    const Cfg cfgs[] = {{"1024 WG x 4 waves, 64 states/round", 1024, 1}, {"1024 WG x 4 waves, 256 states/round", 1024, 4},
-                        {"256 WG x 4 waves, 256 states/round", 256, 4}, {"4096 WG x 4 waves, 256 states/round", 4096, 4}};
+    const Cfg cfgs[] = {{"1024 WG x 4 waves, 256 states/round", 1024, 4}, {"1024 WG x 4 waves, 1024 states/round", 1024, 16},
+                        {"4096 WG x 4 waves, 1024 states/round", 4096, 16}, {"256 WG x 4 waves, 1024 states/round", 256, 16}};
     for (const Cfg& c : cfgs) {
         std::vector<float> tk, tm;
-        for (int rep = 0; rep < 25; ++rep) {
+        for (int rep = 0; rep < 12; ++rep) {
             CK(hipEventRecord(e0, 0));
             CK(hipMemsetAsync(ctr, 0, 4, 0));
             CK(hipMemsetAsync(state, 0, 8 * ntiles, 0));
             CK(hipEventRecord(e1, 0));
             if (c.w == 4) hipLaunchKernelGGL(lookback_kernel<4>, dim3(c.grid), dim3(256), 0, 0, dm, n, bd, ctr, state, base, fail);
-            else hipLaunchKernelGGL(lookback_kernel<1>, dim3(c.grid), dim3(256), 0, 0, dm, n, bd, ctr, state, base, fail);
+            else hipLaunchKernelGGL(lookback_kernel<16>, dim3(c.grid), dim3(256), 0, 0, dm, n, bd, ctr, state, base, fail);
             CK(hipEventRecord(e2, 0));
             CK(hipEventSynchronize(e2));
             float a, b;
