@@ -49,9 +49,11 @@ case $step in
     done
     python3 scripts/sq_json.py $OUT/sq_$wl.json "rocprofv3 --kernel-trace --pmc, 2 passes over bench.py --workload $wl --steps 3 --warmup 1 $*" \
       $(ls $OUT/sq_${wl}_1/*counter_collection.csv) $(ls $OUT/sq_${wl}_2/*counter_collection.csv) | grep onc ;;
-  round)
-    # the round's evidence: default line, every workload, rocprof stats of c1 and c4, FETCH/WRITE traffic
+  round|benches|profs)
+    # the round's evidence: default line, every workload (benches), rocprof stats of c1 and c4,
+    # FETCH/WRITE traffic (profs); round = both
     OUT=$PWD/gpurun_out
+    if [ $step != profs ]; then
     timeout -k 10 600 python -u bench.py > $OUT/bench_default.log 2>&1; rc=$?; echo "bench default rc=$rc"; [ $rc -eq 0 ] || exit $rc
     for wl in c2 c3 c0 c4; do
       timeout -k 10 600 python -u bench.py --workload $wl --c4-leg off > $OUT/bench_$wl.log 2>&1; rc=$?; echo "bench $wl rc=$rc"; [ $rc -eq 0 ] || exit $rc
@@ -60,6 +62,8 @@ case $step in
     for wl in c1 c3 c0; do
       timeout -k 10 400 python -u bench.py --workload $wl --iov --c4-leg off > $OUT/bench_iov_$wl.log 2>&1; rc=$?; echo "bench iov $wl rc=$rc"; [ $rc -eq 0 ] || exit $rc
     done
+    fi
+    [ $step = benches ] && exit 0
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_c1 -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie --c4-leg off --iov-leg off --cache-leg off > $OUT/prof_c1.log 2>&1; rc=$?; echo "rocprof c1 rc=$rc"; [ $rc -eq 0 ] || exit $rc
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_c4 -o run --output-format csv -- python3 bench.py --workload c4 --steps 5 --warmup 1 --no-cpu-baseline > $OUT/prof_c4.log 2>&1; rc=$?; echo "rocprof c4 rc=$rc"; [ $rc -eq 0 ] || exit $rc
     for wl in ${WORKLOADS:-c1 c2 c3 c0 c4}; do
