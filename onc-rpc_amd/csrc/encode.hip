@@ -591,29 +591,35 @@ __device__ __forceinline__ void img_placeholder(uint32_t* img32, ImgSink& w, uin
 // predecessor not yet published re-reads; past kLbSpinLimit rounds it gives
 // up and flags lb_fail (a bound, never a hang).
 constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
-constexpr uint32_t kLbSpinLimit = 1u << 22;
+constexpr uint32_t kLbSpinLimit = 1u << 16;
 #ifndef ONC_LB_W
-#define ONC_LB_W 16
+#define ONC_LB_W 1
+#endif
+#ifndef ONC_LB_W0
+#define ONC_LB_W0 1
 #endif
 constexpr int kLbW = ONC_LB_W;                    // states per lane per round (64 * kLbW per round)
+constexpr int kLbW0 = ONC_LB_W0;                  // the first round's (the nearest predecessors)
 __device__ __forceinline__ uint64_t tile_lookback(const EncArgs& a, uint64_t t, uint64_t agg) {
     const int lane = threadIdx.x & 63;
     if (lane == 0) __hip_atomic_store(a.lb_state + t, kLbAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t excl = 0;
     int64_t j = int64_t(t);                        // tiles [0, j) not summed yet
     uint32_t spins = 0;
+    int w = kLbW0;
     while (j > 0) {
         uint64_t v[kLbW];
 #pragma unroll
         for (int k = 0; k < kLbW; ++k) {
             const int64_t idx = j - 1 - lane - 64 * k;
-            v[k] = idx >= 0 ? __hip_atomic_load(a.lb_state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+            v[k] = idx >= 0 && k < w ? __hip_atomic_load(a.lb_state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : kLbIncl;
         }
         bool done = false, retry = false;
         uint64_t sum = 0;
 #pragma unroll
         for (int k = 0; k < kLbW; ++k) {
-            if (done || retry) continue;
+            if (done || retry || k >= w) continue;
             const uint64_t incl = __ballot((v[k] >> 62) == 2);
             const uint64_t empty = __ballot((v[k] >> 62) == 0);
             const int first = incl ? __builtin_ctzll(incl) : 64;
@@ -634,15 +640,61 @@ __device__ __forceinline__ uint64_t tile_lookback(const EncArgs& a, uint64_t t, 
         }
         excl += sum;
         if (done) break;
-        j -= 64 * kLbW;
+        j -= 64 * w;
+        w = kLbW;
     }
     if (lane == 0) __hip_atomic_store(a.lb_state + t, kLbIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return excl;
 }
 
+// ONC_VARIANT_SP_WG_LOOKBACK (lab, with a workgroup claim or blockIdx
+// order): one look-back per workgroup over workgroup states instead of one
+// per tile — a quarter of the states, read by a quarter of the waves. The
+// waves of the workgroup hand their tile totals to wave 0 through LDS
+// flags (waves whose tile lies past the batch do not take part), wave 0
+// looks back for the workgroup and hands the base back.
+struct WgLb {
+    uint64_t agg[kFastWaves];
+    uint64_t base;
+    uint32_t ready[kFastWaves];     // wave w's total is in agg[w] (w > 0); ready[0]: base is set
+};
+__device__ __forceinline__ uint32_t lds_flag(const uint32_t* f) {
+    return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint64_t wg_lookback(const EncArgs& a, WgLb& X, uint64_t tile, uint64_t agg) {
+    const int lane = threadIdx.x & 63;
+    const int w = int(tile % kFastWaves);
+    const uint64_t g = tile / kFastWaves;
+    const uint64_t ntiles = num_emit_tiles(a.n);
+    const int live = int(min(uint64_t(kFastWaves), ntiles - g * kFastWaves));
+    if (w != 0) {
+        if (lane == 0) {
+            X.agg[w] = agg;
+            __hip_atomic_store(&X.ready[w], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        while (__builtin_amdgcn_readfirstlane(int(lds_flag(&X.ready[0]))) == 0) __builtin_amdgcn_s_sleep(1);
+    } else {
+        uint64_t total = agg;
+        for (int v = 1; v < live; ++v) {
+            while (__builtin_amdgcn_readfirstlane(int(lds_flag(&X.ready[v]))) == 0) __builtin_amdgcn_s_sleep(1);
+            total += X.agg[v];
+        }
+        const uint64_t excl = tile_lookback(a, g, total);
+        if (lane == 0) {
+            X.agg[0] = agg;
+            X.base = excl;
+            __hip_atomic_store(&X.ready[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    uint64_t b = X.base;
+    for (int v = 0; v < w; ++v) b += X.agg[v];
+    return b;
+}
+
 template <int kU, int kNT, bool kFused, bool kRoot = false, bool kGiven = false, bool kPre = false,
           bool kLen = false, bool kSingle = false>
-__device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile, uint64_t given = 0) {
+__device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile, uint64_t given = 0,
+                                              WgLb* X = nullptr) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = tile * kEmitRecs;
     uint32_t* img32 = reinterpret_cast<uint32_t*>(T.img);
@@ -715,7 +767,8 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((payload + d.payload_off) & 3) == 0);
     }
     const uint64_t incl = wave_incl_scan_u64(len);
-    if constexpr (kSingle) T0 = a.origin + launch_base(a) + tile_lookback(a, tile, lane_u64(incl, 63));
+    if constexpr (kSingle)
+        T0 = a.origin + launch_base(a) + (X ? wg_lookback(a, *X, tile, lane_u64(incl, 63)) : tile_lookback(a, tile, lane_u64(incl, 63)));
     const uint64_t start = T0 + incl - len;
     const uint64_t en = start + len;
     const uint64_t pst = start + 4ull * hw;
@@ -1325,10 +1378,33 @@ __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu
     __shared__ ImgTile s_tiles[kFastWaves];
     uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
     if constexpr (kSingle) {
-        // tiles claimed in start order (the claim counter is the word after the tiles' states)
-        uint32_t t = 0;
-        if ((threadIdx.x & 63) == 0) t = atomicAdd(reinterpret_cast<uint32_t*>(a.lb_state + num_emit_tiles(a.n)), 1u);
-        tile = uint32_t(__builtin_amdgcn_readfirstlane(int(t)));
+        // tiles claimed in start order (the claim counter is the word after
+        // the tiles' states): one claim per wave, or (ONC_VARIANT_SP_WG_CLAIM)
+        // one per workgroup for its kFastWaves tiles, or (ONC_VARIANT_SP_BLOCK_ORDER)
+        // none — blockIdx order, which waits only on earlier workgroups if the
+        // dispatcher starts them in order (lab)
+        uint32_t* ctr = reinterpret_cast<uint32_t*>(a.lb_state + num_emit_tiles(a.n));
+        __shared__ WgLb s_lb;
+        const bool wgl = (a.variant & ONC_VARIANT_SP_WG_LOOKBACK) &&
+                         (a.variant & (ONC_VARIANT_SP_WG_CLAIM | ONC_VARIANT_SP_BLOCK_ORDER));
+        if (wgl) {
+            if (threadIdx.x < kFastWaves) s_lb.ready[threadIdx.x] = 0u;
+            __syncthreads();                        // every wave of the workgroup is here
+        }
+        if (a.variant & ONC_VARIANT_SP_WG_CLAIM) {
+            __shared__ uint32_t s_claim;
+            if (threadIdx.x == 0) s_claim = atomicAdd(ctr, 1u);
+            __syncthreads();
+            tile = uint64_t(s_claim) * kFastWaves + (threadIdx.x >> 6);
+        } else if (!(a.variant & ONC_VARIANT_SP_BLOCK_ORDER)) {
+            uint32_t t = 0;
+            if ((threadIdx.x & 63) == 0) t = atomicAdd(ctr, 1u);
+            tile = uint32_t(__builtin_amdgcn_readfirstlane(int(t)));
+        }
+        if (tile < num_emit_tiles(a.n))
+            enc_emit_tile<kU, kNT, kFused, kRoot, false, kPre, kLen, kSingle>(a, s_tiles[threadIdx.x >> 6], tile, 0,
+                                                                              wgl ? &s_lb : nullptr);
+        return;
     }
     if (tile < num_emit_tiles(a.n))
         enc_emit_tile<kU, kNT, kFused, kRoot, false, kPre, kLen, kSingle>(a, s_tiles[threadIdx.x >> 6], tile);
