@@ -380,6 +380,7 @@ typedef struct onc_codec onc_codec;
 #define ONC_VARIANT_SP_WG_CLAIM      0x400000u /* single pass: one tile claim per workgroup (lab) */
 #define ONC_VARIANT_SP_BLOCK_ORDER   0x800000u /* single pass: tiles in blockIdx order, no claim (lab) */
 #define ONC_VARIANT_SP_WG_LOOKBACK   0x1000000u /* single pass: one look-back per workgroup (lab; with one of the two above) */
+#define ONC_VARIANT_SP_WG8          0x2000000u /* single pass: 8 tiles per workgroup, blockIdx order, one look-back each (lab) */
 
 #define ONC_OPT_FORCE_SCAN 0x1u   /* always launch the separate block-scan kernels (tests of that path) */
 

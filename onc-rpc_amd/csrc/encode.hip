@@ -653,20 +653,23 @@ __device__ __forceinline__ uint64_t tile_lookback(const EncArgs& a, uint64_t t, 
 // waves of the workgroup hand their tile totals to wave 0 through LDS
 // flags (waves whose tile lies past the batch do not take part), wave 0
 // looks back for the workgroup and hands the base back.
-struct WgLb {
-    uint64_t agg[kFastWaves];
+template <int kGW>
+struct WgLbT {
+    uint64_t agg[kGW];
     uint64_t base;
-    uint32_t ready[kFastWaves];     // wave w's total is in agg[w] (w > 0); ready[0]: base is set
+    uint32_t ready[kGW];            // wave w's total is in agg[w] (w > 0); ready[0]: base is set
 };
+using WgLb = WgLbT<kFastWaves>;
 __device__ __forceinline__ uint32_t lds_flag(const uint32_t* f) {
     return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ uint64_t wg_lookback(const EncArgs& a, WgLb& X, uint64_t tile, uint64_t agg) {
+template <int kGW>
+__device__ __forceinline__ uint64_t wg_lookback(const EncArgs& a, WgLbT<kGW>& X, uint64_t tile, uint64_t agg) {
     const int lane = threadIdx.x & 63;
-    const int w = int(tile % kFastWaves);
-    const uint64_t g = tile / kFastWaves;
+    const int w = int(tile % kGW);
+    const uint64_t g = tile / kGW;
     const uint64_t ntiles = num_emit_tiles(a.n);
-    const int live = int(min(uint64_t(kFastWaves), ntiles - g * kFastWaves));
+    const int live = int(min(uint64_t(kGW), ntiles - g * kGW));
     if (w != 0) {
         if (lane == 0) {
             X.agg[w] = agg;
@@ -692,9 +695,9 @@ __device__ __forceinline__ uint64_t wg_lookback(const EncArgs& a, WgLb& X, uint6
 }
 
 template <int kU, int kNT, bool kFused, bool kRoot = false, bool kGiven = false, bool kPre = false,
-          bool kLen = false, bool kSingle = false>
+          bool kLen = false, bool kSingle = false, int kGW = kFastWaves>
 __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile, uint64_t given = 0,
-                                              WgLb* X = nullptr) {
+                                              WgLbT<kGW>* X = nullptr) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = tile * kEmitRecs;
     uint32_t* img32 = reinterpret_cast<uint32_t*>(T.img);
@@ -1410,6 +1413,25 @@ __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu
         enc_emit_tile<kU, kNT, kFused, kRoot, false, kPre, kLen, kSingle>(a, s_tiles[threadIdx.x >> 6], tile);
 }
 
+// Single pass with kSpWaves tiles per workgroup (ONC_VARIANT_SP_WG8, lab):
+// blockIdx order and one look-back per workgroup, over half the states the
+// 4-wave workgroups publish (8 image tiles: 2 workgroups per CU by LDS, the
+// same 4 waves per SIMD).
+#ifndef ONC_SP_WAVES
+#define ONC_SP_WAVES 8
+#endif
+constexpr int kSpWaves = ONC_SP_WAVES;
+__global__ __launch_bounds__(64 * kSpWaves) __attribute__((amdgpu_waves_per_eu(4))) void enc_emit_single_kernel(EncArgs a) {
+    __shared__ ImgTile s_tiles[kSpWaves];
+    __shared__ WgLbT<kSpWaves> s_lb;
+    if (threadIdx.x < kSpWaves) s_lb.ready[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint64_t tile = uint64_t(blockIdx.x) * kSpWaves + (threadIdx.x >> 6);
+    if (tile < num_emit_tiles(a.n))
+        enc_emit_tile<kEmitChunkUnroll, kEmitNT, false, false, false, false, false, true, kSpWaves>(
+            a, s_tiles[threadIdx.x >> 6], tile, 0, &s_lb);
+}
+
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
     if (a.root != ONC_ROOT_RPC_MESSAGE)
         ONC_LAUNCH(enc_len_kernel<true>, dim3(uint32_t(num_len_blocks(a.n))), dim3(kLenThreads), 0, s, a);
@@ -1445,6 +1467,11 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     const dim3 g{uint32_t(blocks)}, b{uint32_t(64 * kFastWaves)};
+    if (a.lb_state && (a.variant & ONC_VARIANT_SP_WG8)) {
+        ONC_LAUNCH(enc_emit_single_kernel, dim3(uint32_t((num_emit_tiles(a.n) + kSpWaves - 1) / kSpWaves)),
+                   dim3(64 * kSpWaves), 0, s, a);
+        return hipGetLastError();
+    }
     if (a.lb_state) {                               // (lab: the single pass, codec.hip single_pass)
         ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false, false, false, false, true>), g, b, 0, s, a);
         return hipGetLastError();

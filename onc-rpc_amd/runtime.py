@@ -46,6 +46,7 @@ VARIANT_WS_NO_INTERIOR, VARIANT_WS_NO_FULL, VARIANT_WS_PIPELINE = 0x4000, 0x8000
 VARIANT_EMIT_REPLAN, VARIANT_WHOLE_PLAN, VARIANT_EMIT_PRELOAD = 0x20000, 0x40000, 0x80000
 VARIANT_SINGLE_PASS = 0x200000
 VARIANT_SP_WG_CLAIM, VARIANT_SP_BLOCK_ORDER, VARIANT_SP_WG_LOOKBACK = 0x400000, 0x800000, 0x1000000
+VARIANT_SP_WG8 = 0x2000000
 # options every Codec() gets unless it is given its own (bench.py --variant)
 DEFAULT_OPTIONS: dict = {}
 

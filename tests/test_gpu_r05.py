@@ -367,7 +367,7 @@ def test_c4_device_byte_check_across_chunks(R):
 # ---------------------------------------------------------------------------
 # single pass (ONC_VARIANT_SINGLE_PASS, lab): no enc_len launch
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("claim", ["wave", "workgroup", "block_order", "workgroup_wgl", "block_order_wgl"])
+@pytest.mark.parametrize("claim", ["wave", "workgroup", "block_order", "workgroup_wgl", "block_order_wgl", "wg8"])
 @pytest.mark.parametrize("kind", ["mixed", "unix16", "adversarial", "call_none"])
 def test_single_pass_encode_bit_exact(R, oracle, kind, claim):
     """The single-pass encode (tiles claimed in start order — per wave, per
@@ -382,7 +382,8 @@ def test_single_pass_encode_bit_exact(R, oracle, kind, claim):
           "call_none": lambda: S.call_none(300_000, 256, seed=94)}[kind]()
     extra = {"wave": 0, "workgroup": R.VARIANT_SP_WG_CLAIM, "block_order": R.VARIANT_SP_BLOCK_ORDER,
              "workgroup_wgl": R.VARIANT_SP_WG_CLAIM | R.VARIANT_SP_WG_LOOKBACK,
-             "block_order_wgl": R.VARIANT_SP_BLOCK_ORDER | R.VARIANT_SP_WG_LOOKBACK}[claim]
+             "block_order_wgl": R.VARIANT_SP_BLOCK_ORDER | R.VARIANT_SP_WG_LOOKBACK,
+             "wg8": R.VARIANT_SP_WG8}[claim]
     c = R.Codec(0, variant=R.VARIANT_SINGLE_PASS | extra)
     try:
         o_st, o_len = _enc_oracle_sized(R, c, hb, oracle)
