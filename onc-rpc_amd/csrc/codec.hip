@@ -618,10 +618,42 @@ int single_pass(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out
     return run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
 }
 
+// Small batches (at most one enc_emit_single_kernel workgroup: kSpWaves
+// tiles, 512 records): one launch, no length pass. The workgroup's waves plan their
+// tiles and hand the totals to wave 0 through LDS (encode.hip wg_lookback);
+// the only workgroup has no predecessor, so its look-back reads nothing and
+// the state words need no reset. The per-message loop of a drop-in caller
+// (the C++ mirror's serialise_into) pays one kernel launch instead of two.
+// Variant bits that force an emit kernel keep the two-pass path (tests).
+constexpr uint64_t kSmallRecs = uint64_t(onc::kEmitRecs) * onc::kSpWaves;
+constexpr uint32_t kForcedEmit = ONC_VARIANT_EMIT_WS | ONC_VARIANT_EMIT_TILE | ONC_VARIANT_EMIT_REPLAN |
+                                 ONC_VARIANT_EMIT_PRELOAD | ONC_VARIANT_SINGLE_PASS;
+int small_batch(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
+                int32_t* status, uint32_t* rec_len) {
+    onc::EncArgs a;
+    int rc = enc_args(c, batch, status, rec_len, a);
+    if (rc != ONC_RC_OK) return rc;
+    forget_plan(c);
+    a.ws = 0;
+    a.block_pay = nullptr;
+    a.variant |= ONC_VARIANT_SP_WG8;
+    a.origin = reinterpret_cast<uintptr_t>(out) & 15;
+    a.out = out - a.origin;
+    a.out_cap = out ? a.origin + out_cap : 0;
+    a.rec_off = rec_off;
+    a.rec_len = rec_len;
+    const uint64_t ntiles = onc::num_emit_tiles(batch->n);
+    a.lb_state = c->scratch;                                   // word 0 written, never read
+    a.lb_fail = reinterpret_cast<uint32_t*>(c->scratch + ntiles) + 1;
+    return run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
+}
+
 int encode_batch(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
                  int32_t* status, uint32_t* rec_len, uint32_t root) {
     const uint64_t n = batch->n;
     const uint64_t chunk = c->enc_chunk ? c->enc_chunk : kEncChunk;
+    if (root == ONC_ROOT_RPC_MESSAGE && n <= kSmallRecs && n <= chunk && !(c->variant & kForcedEmit))
+        return small_batch(c, batch, out, out_cap, rec_off, status, rec_len);
     if ((c->variant & ONC_VARIANT_SINGLE_PASS) && root == ONC_ROOT_RPC_MESSAGE && n <= chunk)
         return single_pass(c, batch, out, out_cap, rec_off, status, rec_len);
     if (n <= chunk || (c->variant & ONC_VARIANT_WHOLE_PLAN)) {     // whole-batch plan (lab)

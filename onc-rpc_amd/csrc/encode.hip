@@ -1417,10 +1417,6 @@ __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu
 // blockIdx order and one look-back per workgroup, over half the states the
 // 4-wave workgroups publish (8 image tiles: 2 workgroups per CU by LDS, the
 // same 4 waves per SIMD).
-#ifndef ONC_SP_WAVES
-#define ONC_SP_WAVES 8
-#endif
-constexpr int kSpWaves = ONC_SP_WAVES;
 __global__ __launch_bounds__(64 * kSpWaves) __attribute__((amdgpu_waves_per_eu(4))) void enc_emit_single_kernel(EncArgs a) {
     __shared__ ImgTile s_tiles[kSpWaves];
     __shared__ WgLbT<kSpWaves> s_lb;

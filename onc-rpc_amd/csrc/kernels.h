@@ -190,5 +190,12 @@ hipError_t launch_dlen_tiles(const uint32_t* rec_len, uint64_t n, uint64_t* tile
 __host__ __device__ inline uint64_t num_tiles(uint64_t n) { return (n + 255) / 256; }
 __host__ __device__ inline uint64_t num_len_blocks(uint64_t n) { return (n + kLenRecs - 1) / kLenRecs; }
 __host__ __device__ inline uint64_t num_emit_tiles(uint64_t n) { return (n + kEmitRecs - 1) / kEmitRecs; }
+// enc_emit_single_kernel: tiles (waves) per workgroup — the single pass's
+// look-back granule, and the size of the one-launch small-batch encode
+// (kSpWaves * kEmitRecs records: one workgroup, nothing to look back over)
+#ifndef ONC_SP_WAVES
+#define ONC_SP_WAVES 8
+#endif
+constexpr int kSpWaves = ONC_SP_WAVES;
 
 }  // namespace onc

@@ -392,3 +392,28 @@ def test_single_pass_encode_bit_exact(R, oracle, kind, claim):
         _enc_oracle_sized(R, c, hb, oracle, shift=3, cap=total // 3 + 7)
     finally:
         c.close()
+
+
+# ---------------------------------------------------------------------------
+# small batches (<= 512 records): one enc_emit_single_kernel launch, no
+# length pass (codec.hip small_batch) — the default path, every content kind
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 300, 511, 512, 513])
+def test_small_batch_one_launch_bit_exact(R, oracle, n):
+    """Batches up to 512 records encode in one launch (the workgroup's waves
+    place their tiles through LDS); at and around the tile and workgroup
+    boundaries they give the oracle's bytes, offsets, statuses and lengths for
+    adversarial content (failing and declared AUTH_UNIX records, placeholders)
+    and for configs[0]'s message, at two writer positions and with a capacity
+    inside the batch; 513 records take the two-pass path."""
+    from test_gpu_emit_paths import _enc_oracle_sized, _adversarial
+    c = R.Codec(0)
+    try:
+        for hb in (_adversarial(97 + n, n=n), S.cpu_roundtrip(n)):
+            o_st, o_len = _enc_oracle_sized(R, c, hb, oracle)
+            _enc_oracle_sized(R, c, hb, oracle, shift=7)
+            total = int(o_len.astype(np.int64).sum())
+            if total > 8:
+                _enc_oracle_sized(R, c, hb, oracle, shift=1, cap=total // 2 + 3)
+    finally:
+        c.close()
