@@ -904,10 +904,16 @@ int onc_decode_lengths(onc_codec* c, const uint8_t* wire, const uint32_t* rec_le
     a.base = base;
     a.rec_off_out = rec_off;
     uint64_t* blk_sum = c->scratch + 3 * T;
-    rc = run(c, ONC_K_LEN_TILES, "dlen_tiles", [&] {
-        return onc::launch_dlen_tiles(rec_len, n, c->scratch, blk_sum, c->stream);
-    });
-    if (rc != ONC_RC_OK) return rc;
+    // one decode workgroup (n <= 64): its offsets are its own wave scan of
+    // the lengths from `base` — the totals of earlier workgroups and blocks
+    // it would read are masked to 0 (decode.hip kFromLen), so no dlen_tiles
+    // launch (a single message's try_from pays one launch)
+    if (wgs > 1 || c->force_scan) {
+        rc = run(c, ONC_K_LEN_TILES, "dlen_tiles", [&] {
+            return onc::launch_dlen_tiles(rec_len, n, c->scratch, blk_sum, c->stream);
+        });
+        if (rc != ONC_RC_OK) return rc;
+    }
     if (nblk > onc::kDecLenFusedBlocks || c->force_scan) {
         uint64_t* blk_base = blk_sum + (T / 4 + 1);
         rc = run(c, ONC_K_SCAN_TILES, "scan_tiles",

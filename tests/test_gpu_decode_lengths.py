@@ -96,3 +96,26 @@ def test_decode_lengths_same_as_scan_then_decode(codec, R, oracle, n):
         assert np.array_equal(g_off, o_off)
         for k in (0, 2, 3, 4):          # unix slots are defined only for AUTH_UNIX records
             assert np.array_equal(np.asarray(g[k]).view(np.uint8), np.asarray(h[k]).view(np.uint8)), k
+
+
+@pytest.mark.parametrize("n", [1, 2, 33, 64])
+def test_decode_lengths_one_workgroup(codec, R, oracle, n):
+    """One decode workgroup (n <= 64) launches the decode alone (no
+    dlen_tiles): offsets from its own scan, at a non-zero base, corrupted
+    records included, equal to the oracle in both modes."""
+    hb = S.mixed(n, seed=70 + n, pmin=0, pmax=300, exotic=0.3)
+    o_wire, o_off, _, _ = oracle.encode_batch(hb)
+    w, off = S.corrupt(np.frombuffer(o_wire, np.uint8), o_off, frac=0.2, seed=71 + n)
+    base = 5
+    wire = bytes(base) + w.tobytes()
+    lens = np.diff(off.astype(np.int64)).astype(np.uint32)
+    for mode in MODES:
+        g, g_off = _decode_lengths(R, codec, wire, lens, base, mode)
+        o = oracle.decode_batch(np.frombuffer(wire + b"\0" * 16, np.uint8).copy(), off.astype(np.uint64) + np.uint64(base),
+                                mode)
+        assert np.array_equal(g_off, off.astype(np.uint64) + np.uint64(base))
+        assert np.array_equal(g[2], o[2]) and np.array_equal(g[3], o[3]) and np.array_equal(g[4], o[4])
+        assert np.array_equal(g[0].view(np.uint8), o[0].view(np.uint8))
+        _, gp = L.resolve_unix(g[0], g[1], g[2])
+        _, op = L.resolve_unix(o[0], o[1], o[2])
+        assert np.array_equal(gp, op)
