@@ -502,7 +502,10 @@ int onc_encode_lengths(onc_codec* codec, const onc_batch* batch,
  *                      keeps its declared extent as a framable placeholder
  *                      (onc_auth). Bytes at or beyond out_cap are never
  *                      written; records ending beyond it get ONC_ENC_WRITE_ZERO.
- *   rec_len[dev, n]  : optional (may be NULL) serialised lengths. */
+ *   rec_len[dev, n]  : optional (may be NULL) serialised lengths.
+ * Launches: a length pass and the emit per 1M-record chunk; a batch of at
+ * most 512 records is planned and emitted in one launch (the results are the
+ * same). */
 int onc_encode(onc_codec* codec, const onc_batch* batch,
                uint8_t* out, uint64_t out_cap,
                uint64_t* rec_off, int32_t* status, uint32_t* rec_len);
@@ -524,7 +527,8 @@ int onc_encode(onc_codec* codec, const onc_batch* batch,
  * plan (then ONC_RC_EINVAL too). The descriptors must not change in between,
  * nor the plan's rec_len array when one was given (for a batch with an
  * AUTH_UNIX table the emit reads the record lengths back from it instead of
- * re-planning). onc_encode = plan + emit. */
+ * re-planning). onc_encode = plan + emit (for more than 512 records; a
+ * smaller batch it encodes in one launch). */
 int onc_encode_plan(onc_codec* codec, const onc_batch* batch, int32_t* status, uint32_t* rec_len);
 int onc_encode_emit(onc_codec* codec, const onc_batch* batch, uint8_t* out, uint64_t out_cap,
                     uint64_t* rec_off, int32_t* status);
