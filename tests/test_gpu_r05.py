@@ -417,3 +417,29 @@ def test_small_batch_one_launch_bit_exact(R, oracle, n):
                 _enc_oracle_sized(R, c, hb, oracle, shift=1, cap=total // 2 + 3)
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("n", [3, 200, 512, 600])
+def test_small_batch_capacity_zero_and_tiny(R, oracle, n):
+    """onc_encode with no output room (out_cap 0) and with room for a few
+    bytes: every record that does not fit gets ONC_ENC_WRITE_ZERO and the
+    offsets still place every record — on the one-launch path (n <= 512) as
+    on the two-pass one, against the oracle."""
+    import torch
+    hb = S.cpu_roundtrip(n)
+    db = R.DeviceBatch.from_host(hb)
+    c = R.Codec(0)
+    try:
+        for cap in (0, 5, 200):
+            o_wire, o_off, o_st, o_len = oracle.encode_batch(hb, out_cap=cap)
+            buf = torch.full((cap + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+            off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+            st = torch.empty(n, dtype=torch.int32, device="cuda")
+            c.encode(db, buf, off, st, out_cap=cap)
+            c.sync()
+            assert np.array_equal(st.cpu().numpy(), o_st)
+            assert np.array_equal(off.cpu().numpy().view(np.uint64), o_off)
+            b = buf.cpu().numpy()
+            assert b[:len(o_wire)].tobytes() == o_wire and (b[cap:] == 0x5A).all()
+    finally:
+        c.close()
