@@ -65,7 +65,13 @@ extern "C" {
  *    stays framable (onc_encode_iov emits the same placeholder as its header
  *    iovec); onc_host_register / onc_host_unregister map a caller's host
  *    buffer (a socket buffer) for the kernels to read and write in place. */
-#define ONC_RPC_ABI_VERSION 7
+/* 8: onc_compact / onc_compact_iov (a failing record's extent dropped from an
+ *    encoded batch: the stream the reference's per-message loop writes);
+ *    timing id ONC_K_COMPACT; onc_host_unregister takes a NULL codec and
+ *    registrations are counted per range (a pinned range belongs to the
+ *    process); the rejected-experiment variant bits (EMIT_PRELOAD,
+ *    DEC_AUX_SPARSE, SINGLE_PASS, SP_*) are gone. */
+#define ONC_RPC_ABI_VERSION 8
 
 /* ------------------------------------------------------------------------ */
 /* Wire discriminants (values are the on-wire u32s)                          */
@@ -371,16 +377,6 @@ typedef struct onc_codec onc_codec;
 #define ONC_VARIANT_WS_PIPELINE      0x10000u  /* wave-specialised: the pipeline on header-heavy batches too */
 #define ONC_VARIANT_EMIT_REPLAN      0x20000u  /* wave-per-tile enc_emit re-plans instead of reading the plan's lengths */
 #define ONC_VARIANT_WHOLE_PLAN       0x40000u  /* plan a large batch whole instead of in chunks */
-#define ONC_VARIANT_EMIT_PRELOAD     0x80000u  /* wave-per-tile enc_emit: preload the AUTH_UNIX credential block (lab) */
-#define ONC_VARIANT_DEC_AUX_SPARSE   0x100000u /* decode: aux0/aux1 written only for failing records (lab;
-                                                  the outputs of OK records' aux words are then undefined) */
-#define ONC_VARIANT_SINGLE_PASS      0x200000u /* onc_encode without the length pass: the wave-per-tile
-                                                  enc_emit claims tiles in start order and places them by a
-                                                  decoupled look-back (lab; one plan chunk, RpcMessage root) */
-#define ONC_VARIANT_SP_WG_CLAIM      0x400000u /* single pass: one tile claim per workgroup (lab) */
-#define ONC_VARIANT_SP_BLOCK_ORDER   0x800000u /* single pass: tiles in blockIdx order, no claim (lab) */
-#define ONC_VARIANT_SP_WG_LOOKBACK   0x1000000u /* single pass: one look-back per workgroup (lab; with one of the two above) */
-#define ONC_VARIANT_SP_WG8          0x2000000u /* single pass: 8 tiles per workgroup, blockIdx order, one look-back each (lab) */
 
 #define ONC_OPT_FORCE_SCAN 0x1u   /* always launch the separate block-scan kernels (tests of that path) */
 
@@ -422,14 +418,22 @@ int onc_codec_reserve(onc_codec* codec, uint64_t max_records);
  * zero-copy counterpart of the reference's borrowed slices
  * (call_body.rs:53-59, opaque.rs:92-97): onc_decode of a registered wire
  * fetches only the 16-byte granules holding the header bytes it parses over
- * the link, never the payloads. Synchronous. A range already pinned by
- * hipHostMalloc (or torch's pin_memory) needs no registration: its device
- * address is returned and nothing is registered (onc_host_unregister of it
- * is then a no-op). The address is for the codec's device. Returns
- * ONC_RC_EINVAL for a NULL pointer or length, ONC_RC_EHIP if the runtime
- * refuses the range (onc_codec_last_error says why). */
+ * the link, never the payloads. Synchronous. A pinned range belongs to the
+ * process, not to the codec (destroying the codec leaves it pinned): a
+ * register of a range inside one this library pinned maps it and counts one
+ * more registration of that range; each onc_host_unregister counts one
+ * down and the last unpins it. A range already pinned by its owner
+ * (hipHostMalloc, torch's pin_memory) needs no registration: its device
+ * address is returned and nothing is recorded (onc_host_unregister of it is
+ * then a no-op). The address is for the codec's device. Returns
+ * ONC_RC_EINVAL for a NULL pointer or length, or for a range that starts in
+ * pinned memory but runs past that pinned allocation; ONC_RC_EHIP if the
+ * runtime refuses the range (onc_codec_last_error says why). */
 int onc_host_register(onc_codec* codec, void* host, uint64_t len, void** dev_ptr);
-/* Unpin a range onc_host_register pinned (the kernels must be done with it). */
+/* Undo one onc_host_register of a range this library pinned (`host`: any
+ * address inside it; the kernels must be done with it); the last one unpins
+ * the range. `codec` may be NULL (it is only where an error is reported):
+ * a registration may outlive the codec that made it. */
 int onc_host_unregister(onc_codec* codec, void* host);
 
 /* Last HIP error string seen by this handle ("" if none). */
@@ -464,7 +468,8 @@ int onc_abi_version(void);
 #define ONC_K_FRAME_WALK   10
 #define ONC_K_FRAME_COUNTS 11
 #define ONC_K_FRAME_GUESS  12
-#define ONC_K_COUNT        13
+#define ONC_K_COMPACT      13
+#define ONC_K_COUNT        14
 #define ONC_TIMING_ALL    (-1)
 int onc_codec_enable_timing(onc_codec* codec, int enable);
 int onc_codec_kernel_stats(onc_codec* codec, double* ms_total /*[ONC_K_COUNT]*/,
@@ -561,6 +566,29 @@ typedef struct onc_iov_rec {
 int onc_encode_iov(onc_codec* codec, const onc_batch* batch,
                    uint8_t* hdr_out, uint64_t hdr_cap,
                    onc_iov_rec* iov, int32_t* status, uint64_t* totals);
+
+/* Drop the extent of every record whose status != ONC_OK from a buffer
+ * onc_encode wrote, in place: afterwards out[rec_off[i], rec_off[i+1]) is
+ * record i for an OK record and empty for any other, the OK records back to
+ * back from rec_off[0] (unchanged) on — the bytes the reference's loop of
+ * serialise_into calls on one Cursor<Vec<u8>> writes for the same messages,
+ * since a message that panics (unix_params.rs:47,149, flavor.rs:110) or
+ * fails writes nothing. Only placeholders (a declared AUTH_UNIX credential
+ * failing its deferred block check, onc_auth) have an extent to drop; every
+ * other failing record already takes 0 bytes, so a batch without a
+ * placeholder moves nothing. `status` is onc_encode's. Bytes from the new
+ * rec_off[n] up to the old one are left as they were. *total (host,
+ * optional) receives the new rec_off[n]. Synchronous (it sizes its scratch
+ * by the moved bytes, which it reads back): ONC_RC_ECAPTURE inside a stream
+ * capture. Launches only when the caller saw a failing status. */
+int onc_compact(onc_codec* codec, uint8_t* out, uint64_t* rec_off, const int32_t* status, uint64_t n,
+                uint64_t* total);
+
+/* The same for onc_encode_iov's list: every entry whose status != ONC_OK
+ * gets hdr_len = payload_len = 0 and every wire_off is the kept bytes before
+ * it (rec_off[0] = 0); hdr_off / payload_off are kept. totals[dev, 2]
+ * (optional): {kept header bytes, kept wire bytes}. Asynchronous. */
+int onc_compact_iov(onc_codec* codec, onc_iov_rec* iov, const int32_t* status, uint64_t n, uint64_t* totals);
 
 /* ------------------------------------------------------------------------ */
 /* Decode — RpcMessage::try_from(&[u8]) / try_from(Bytes)                    */

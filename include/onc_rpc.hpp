@@ -46,6 +46,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -463,23 +464,26 @@ public:
     // memory) — no device allocation, no copy calls, one stream
     // synchronisation per call. `host` and `dev` address the same bytes;
     // valid until the next stage() call on this codec (every mirror call
-    // synchronises before it returns).
+    // synchronises before it returns). A stage that grows keeps its first
+    // `keep` bytes (they move with it: re-derive pointers from offsets).
     struct Stage {
         uint8_t* host;
         uint8_t* dev;
     };
-    Stage stage(size_t n) {
+    size_t stage_capacity() const { return stage_cap_; }
+    Stage stage(size_t n, size_t keep = 0) {
         if (n > stage_cap_) {
             size_t want = stage_cap_ ? stage_cap_ : (size_t(1) << 20);
             while (want < n) want *= 2;
+            void* h = nullptr;
+            if (hipHostMalloc(&h, want, hipHostMallocMapped) != hipSuccess) throw CodecError("hipHostMalloc(stage)");
             if (stage_host_) {
                 sync();
+                if (keep) std::memcpy(h, stage_host_, std::min(keep, stage_cap_));
                 (void)hipHostFree(stage_host_);
                 stage_host_ = stage_dev_ = nullptr;
                 stage_cap_ = 0;
             }
-            void* h = nullptr;
-            if (hipHostMalloc(&h, want, hipHostMallocMapped) != hipSuccess) throw CodecError("hipHostMalloc(stage)");
             void* d = nullptr;
             if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
                 (void)hipHostFree(h);
@@ -985,6 +989,15 @@ inline std::vector<int32_t> BatchEncoder::serialise_into(Codec& codec, std::vect
                     "onc_encode_body");
         codec.sync();
         std::memcpy(st.data(), ds.host, n * 4);
+        // a failing message writes nothing (the reference panics or returns
+        // before its first write): placeholder extents dropped (ABI 8)
+        for (size_t i = 0; i < n; ++i) {
+            if (st[i] != ONC_OK) {
+                uint64_t kept = 0;
+                codec.check(onc_compact(codec.get(), dout.dev, doff.dev, ds.dev, n, &kept), "onc_compact");
+                break;
+            }
+        }
         std::memcpy(off.data(), doff.host, (n + 1) * 8);
         const uint64_t total = off[n];
         out.insert(out.end(), dout.host, dout.host + total);
@@ -1105,15 +1118,20 @@ inline std::vector<Decoded> BatchDecoder::stream_at(Codec& codec, const uint8_t*
                                                     size_t wire_len, DecodeMode mode, size_t* consumed,
                                                     std::optional<Error>* stop) {
     using detail::need;
-    const size_t max_records = wire_len / 4 + 1;   // every record is at least 4 bytes
+    // framed first with only the wire, the offsets (every record is at least
+    // 4 bytes) and the result words staged; the decode outputs are carved
+    // for the framed count afterwards (sized for max_records they would be
+    // ~67 bytes of pinned memory per wire byte)
+    const size_t max_records = wire_len / 4 + 1;
     detail::Carve c{codec.stage((dev_wire ? 0 : need<uint8_t>(wire_len)) + need<uint64_t>(max_records + 1) +
-                                need<uint64_t>(5) + out_bytes(max_records))};
+                                need<uint64_t>(5))};
     const uint8_t* wd = dev_wire;
     if (!dev_wire) {
         const auto w = c.take<uint8_t>(wire_len);
         if (wire_len) std::memcpy(w.host, wire, wire_len);
         wd = w.dev;
     }
+    const size_t off_at = c.off;
     const auto off = c.take<uint64_t>(max_records + 1);
     const auto res = c.take<uint64_t>(5);
     codec.check(onc_frame_stream(codec.get(), wd, wire_len, off.dev, max_records, res.dev), "onc_frame_stream");
@@ -1127,9 +1145,15 @@ inline std::vector<Decoded> BatchDecoder::stream_at(Codec& codec, const uint8_t*
     }
     const size_t n = size_t(r[0]);
     if (!n) return {};
+    // the outputs after what is staged (a stage that grows keeps the staged
+    // wire and offsets; their device addresses move with it)
+    const size_t mark = c.off;
+    c.s = codec.stage(mark + out_bytes(n), mark);
+    if (!dev_wire) wd = c.s.dev;
+    const uint64_t* offd = reinterpret_cast<const uint64_t*>(c.s.dev + off_at);
     const Out o = take_out(c, n);
     const onc_decoded d = o.dev();
-    codec.check(onc_decode(codec.get(), wd, off.dev, n, int(mode), &d), "onc_decode");
+    codec.check(onc_decode(codec.get(), wd, offd, n, int(mode), &d), "onc_decode");
     codec.sync();
     return results(o, n, wire);
 }

@@ -10,7 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
-#include <set>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -46,6 +46,12 @@ struct onc_codec {
     const uint32_t* planned_lens = nullptr;
     uint32_t* lens = nullptr;      // codec-owned record lengths (per plan chunk)
     uint64_t lens_cap = 0;
+    // onc_compact / onc_compact_iov: the new offsets (+ the first dropped
+    // record's index in the word after them) and the moved bytes
+    uint64_t* cmp_off = nullptr;
+    uint64_t cmp_off_cap = 0;     // records
+    uint8_t* cmp_bytes = nullptr;
+    uint64_t cmp_bytes_cap = 0;
     uint32_t timing = 0;   // bitmask of ONC_K_* ids whose launches are bracketed
     struct Pending {
         int kernel;
@@ -143,6 +149,28 @@ int ensure_lens(onc_codec* c, uint64_t n) {
     if (hipMalloc(&c->lens, want * sizeof(uint32_t)) != hipSuccess) return ONC_RC_ENOMEM;
     c->lens_cap = want;
     forget_plan(c);
+    return ONC_RC_OK;
+}
+
+// Grows a codec-owned device buffer (outside a capture), keeping nothing.
+template <class T>
+int ensure_buf(onc_codec* c, T*& p, uint64_t& cap, uint64_t want_elems, const char* what) {
+    if (want_elems <= cap) return ONC_RC_OK;
+    if (capturing(c)) return refuse_in_capture(c);
+    uint64_t want = cap ? cap : 65536;
+    while (want < want_elems) want *= 2;
+    if (p) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    const hipError_t e = hipMalloc(&p, want * sizeof(T));
+    if (e != hipSuccess) {
+        fail(c, e, what);
+        return ONC_RC_ENOMEM;
+    }
+    cap = want;
     return ONC_RC_OK;
 }
 
@@ -257,6 +285,8 @@ int onc_codec_destroy(onc_codec* c) {
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->frame_scratch) (void)hipFree(c->frame_scratch);
     if (c->lens) (void)hipFree(c->lens);
+    if (c->cmp_off) (void)hipFree(c->cmp_off);
+    if (c->cmp_bytes) (void)hipFree(c->cmp_bytes);
     if (c->dec_hint_host) (void)hipHostFree(c->dec_hint_host);
     delete c;
     return ONC_RC_OK;
@@ -292,53 +322,96 @@ int onc_codec_reserve(onc_codec* c, uint64_t max_records) {
     return ensure_lens(c, max_records);
 }
 
-// Host ranges onc_host_register pinned (and may unpin): a range that was
-// already pinned by its owner (hipHostMalloc) is mapped but not recorded.
+// Host ranges onc_host_register pinned, process-wide (a pinned range belongs
+// to no codec: hipHostRegister is per process): start -> {length, count}.
+// A register of an address inside one of them maps it and counts it once
+// more; each unregister of an address inside it counts down, the last one
+// unpins. Memory pinned by its owner (hipHostMalloc, torch pin_memory) is
+// mapped and never recorded, so unregistering it does nothing.
+struct HostPin {
+    uint64_t len;
+    uint64_t count;
+};
 static std::mutex g_host_mu;
-static std::set<void*> g_host_pinned;
+static std::map<uintptr_t, HostPin> g_host_pinned;
+
+// the recorded range holding [p, p + len) (len 0: holding p), or end()
+static std::map<uintptr_t, HostPin>::iterator pinned_range(uintptr_t p, uint64_t len) {
+    auto it = g_host_pinned.upper_bound(p);
+    if (it == g_host_pinned.begin()) return g_host_pinned.end();
+    --it;
+    const uint64_t end = it->first + it->second.len;
+    return p < end && p + len <= end ? it : g_host_pinned.end();
+}
 
 int onc_host_register(onc_codec* c, void* host, uint64_t len, void** dev_ptr) {
     if (!c || !host || !len || !dev_ptr) return ONC_RC_EINVAL;
     *dev_ptr = nullptr;
     if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
     std::lock_guard<std::mutex> lk(g_host_mu);
-    // memory the runtime already pinned (hipHostMalloc, a registered range):
-    // only map it (hipHostRegister refuses it)
+    const uintptr_t p = reinterpret_cast<uintptr_t>(host);
+    auto mine = g_host_pinned.end();
     hipPointerAttribute_t attr{};
     bool pinned = false;
     if (hipPointerGetAttributes(&attr, host) == hipSuccess) pinned = attr.type == hipMemoryTypeHost;
     else (void)hipGetLastError();                 // an ordinary host pointer
-    bool mine = false;
-    if (!pinned) {
+    if (pinned) {
+        // inside a range this library pinned: counted once more; inside
+        // memory its owner pinned: the whole [host, host + len) must lie in
+        // that allocation (else a kernel would fault past its end)
+        mine = pinned_range(p, len);
+        if (mine == g_host_pinned.end()) {
+            // (a range inside one registered here but running past it is
+            // refused the same way: it is not one pinned allocation)
+            if (pinned_range(p, 0) != g_host_pinned.end()) {
+                c->last_error = "onc_host_register: range runs past the pinned range holding its start";
+                return ONC_RC_EINVAL;
+            }
+            void* base = nullptr;
+            size_t size = 0;
+            if (hipMemGetAddressRange(reinterpret_cast<hipDeviceptr_t*>(&base), &size, host) == hipSuccess) {
+                const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+                if (p < b || p + len > b + size) {
+                    c->last_error = "onc_host_register: range runs past its pinned allocation";
+                    return ONC_RC_EINVAL;
+                }
+            } else {
+                (void)hipGetLastError();             // no range known: mapped as the runtime reports it
+            }
+        }
+    } else {
         const hipError_t r = hipHostRegister(host, size_t(len), hipHostRegisterMapped | hipHostRegisterPortable);
         if (r == hipSuccess) {
-            mine = true;
+            mine = g_host_pinned.emplace(p, HostPin{len, 0}).first;
         } else if (r == hipErrorHostMemoryAlreadyRegistered) {
-            (void)hipGetLastError();
+            (void)hipGetLastError();                 // pinned by its owner: only mapped
         } else {
             (void)hipGetLastError();
             return fail(c, r, "hipHostRegister");
         }
     }
-    hipError_t e;
-    e = hipHostGetDevicePointer(dev_ptr, host, 0);
+    const hipError_t e = hipHostGetDevicePointer(dev_ptr, host, 0);
     if (e != hipSuccess) {
-        if (mine) (void)hipHostUnregister(host);
+        if (mine != g_host_pinned.end() && mine->second.count == 0) {
+            (void)hipHostUnregister(reinterpret_cast<void*>(mine->first));
+            g_host_pinned.erase(mine);
+        }
         *dev_ptr = nullptr;
         return fail(c, e, "hipHostGetDevicePointer");
     }
-    if (mine) g_host_pinned.insert(host);
+    if (mine != g_host_pinned.end()) ++mine->second.count;
     return ONC_RC_OK;
 }
 
 int onc_host_unregister(onc_codec* c, void* host) {
-    if (!c || !host) return ONC_RC_EINVAL;
-    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    if (!host) return ONC_RC_EINVAL;
     std::lock_guard<std::mutex> lk(g_host_mu);
-    const auto it = g_host_pinned.find(host);
+    const auto it = pinned_range(reinterpret_cast<uintptr_t>(host), 0);
     if (it == g_host_pinned.end()) return ONC_RC_OK;      // not pinned here: nothing to undo
+    if (--it->second.count != 0) return ONC_RC_OK;        // still mapped by another registration
+    void* start = reinterpret_cast<void*>(it->first);
     g_host_pinned.erase(it);
-    const hipError_t e = hipHostUnregister(host);
+    const hipError_t e = hipHostUnregister(start);
     return e == hipSuccess ? ONC_RC_OK : fail(c, e, "hipHostUnregister");
 }
 
@@ -385,6 +458,7 @@ const char* onc_kernel_name(int k) {
         case ONC_K_FRAME_WALK: return "frame_walk_kernel";
         case ONC_K_FRAME_COUNTS: return "frame_counts_kernel";
         case ONC_K_FRAME_GUESS: return "frame_guess_kernel";
+        case ONC_K_COMPACT: return "compact_kernels";
         default: return "?";
     }
 }
@@ -592,42 +666,14 @@ int enc_emit(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_ca
 // offset from rec_off[k's end], which chunk k's emit wrote.
 constexpr uint64_t kEncChunk = onc::kFusedBlocks * onc::kLenRecs;   // 1M records
 
-// ONC_VARIANT_SINGLE_PASS (lab): no enc_len launch — the wave-per-tile
-// enc_emit plans its tiles and places them by a decoupled look-back over
-// per-tile words in the scratch (encode.hip tile_lookback), zeroed by one
-// fill before the launch: the states of the tiles, then the claim counter
-// and the give-up flag.
-int single_pass(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
-                int32_t* status, uint32_t* rec_len) {
-    onc::EncArgs a;
-    int rc = enc_args(c, batch, status, rec_len, a);
-    if (rc != ONC_RC_OK) return rc;
-    forget_plan(c);
-    a.ws = 0;
-    a.block_pay = nullptr;
-    a.origin = reinterpret_cast<uintptr_t>(out) & 15;
-    a.out = out - a.origin;
-    a.out_cap = out ? a.origin + out_cap : 0;
-    a.rec_off = rec_off;
-    a.rec_len = rec_len;
-    const uint64_t ntiles = onc::num_emit_tiles(batch->n);
-    a.lb_state = c->scratch;                                   // ntiles + 1 words (< 3T)
-    a.lb_fail = reinterpret_cast<uint32_t*>(c->scratch + ntiles) + 1;
-    const hipError_t e = hipMemsetAsync(a.lb_state, 0, (ntiles + 1) * sizeof(uint64_t), c->stream);
-    if (e != hipSuccess) return fail(c, e, "hipMemsetAsync");
-    return run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
-}
-
 // Small batches (at most one enc_emit_single_kernel workgroup: kSpWaves
-// tiles, 512 records): one launch, no length pass. The workgroup's waves plan their
-// tiles and hand the totals to wave 0 through LDS (encode.hip wg_lookback);
-// the only workgroup has no predecessor, so its look-back reads nothing and
-// the state words need no reset. The per-message loop of a drop-in caller
+// tiles, 512 records): one launch, no length pass. The workgroup's waves plan
+// their tiles and hand the totals to wave 0 through LDS (encode.hip
+// wg_place); nothing outside the workgroup is read or waited on. The per-message loop of a drop-in caller
 // (the C++ mirror's serialise_into) pays one kernel launch instead of two.
 // Variant bits that force an emit kernel keep the two-pass path (tests).
 constexpr uint64_t kSmallRecs = uint64_t(onc::kEmitRecs) * onc::kSpWaves;
-constexpr uint32_t kForcedEmit = ONC_VARIANT_EMIT_WS | ONC_VARIANT_EMIT_TILE | ONC_VARIANT_EMIT_REPLAN |
-                                 ONC_VARIANT_EMIT_PRELOAD | ONC_VARIANT_SINGLE_PASS;
+constexpr uint32_t kForcedEmit = ONC_VARIANT_EMIT_WS | ONC_VARIANT_EMIT_TILE | ONC_VARIANT_EMIT_REPLAN;
 int small_batch(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out_cap, uint64_t* rec_off,
                 int32_t* status, uint32_t* rec_len) {
     onc::EncArgs a;
@@ -636,15 +682,12 @@ int small_batch(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t out
     forget_plan(c);
     a.ws = 0;
     a.block_pay = nullptr;
-    a.variant |= ONC_VARIANT_SP_WG8;
+    a.small = 1;
     a.origin = reinterpret_cast<uintptr_t>(out) & 15;
     a.out = out - a.origin;
     a.out_cap = out ? a.origin + out_cap : 0;
     a.rec_off = rec_off;
     a.rec_len = rec_len;
-    const uint64_t ntiles = onc::num_emit_tiles(batch->n);
-    a.lb_state = c->scratch;                                   // word 0 written, never read
-    a.lb_fail = reinterpret_cast<uint32_t*>(c->scratch + ntiles) + 1;
     return run(c, ONC_K_ENC_EMIT, "enc_emit", [&] { return onc::launch_enc_emit(a, c->stream); });
 }
 
@@ -654,8 +697,6 @@ int encode_batch(onc_codec* c, const onc_batch* batch, uint8_t* out, uint64_t ou
     const uint64_t chunk = c->enc_chunk ? c->enc_chunk : kEncChunk;
     if (root == ONC_ROOT_RPC_MESSAGE && n <= kSmallRecs && n <= chunk && !(c->variant & kForcedEmit))
         return small_batch(c, batch, out, out_cap, rec_off, status, rec_len);
-    if ((c->variant & ONC_VARIANT_SINGLE_PASS) && root == ONC_ROOT_RPC_MESSAGE && n <= chunk)
-        return single_pass(c, batch, out, out_cap, rec_off, status, rec_len);
     if (n <= chunk || (c->variant & ONC_VARIANT_WHOLE_PLAN)) {     // whole-batch plan (lab)
         const int rc = enc_plan(c, batch, status, rec_len, root);
         if (rc != ONC_RC_OK) return rc;
@@ -1000,6 +1041,76 @@ int onc_encode_body(onc_codec* c, int root, const onc_batch* batch, uint8_t* out
         return e == hipSuccess ? ONC_RC_OK : fail(c, e, "hipMemsetAsync");
     }
     return encode_batch(c, batch, out, out_cap, rec_off, status, rec_len, uint32_t(root));
+}
+
+int onc_compact(onc_codec* c, uint8_t* out, uint64_t* rec_off, const int32_t* status, uint64_t n, uint64_t* total) {
+    if (!c || !rec_off || (n && (!status || !out))) return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    if (capturing(c)) return refuse_in_capture(c);    // synchronous: sizes its scratch from the batch
+    hipError_t e;
+    if (n == 0) {
+        if (total) {
+            e = hipMemcpyAsync(total, rec_off, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            if (e != hipSuccess) return fail(c, e, "hipMemcpyAsync");
+        }
+        return ONC_RC_OK;
+    }
+    int rc = ensure_lens(c, n);
+    if (rc == ONC_RC_OK) rc = ensure_buf(c, c->cmp_off, c->cmp_off_cap, n + 2, "hipMalloc(compact offsets)");
+    if (rc != ONC_RC_OK) return rc;
+    forget_plan(c);
+    uint64_t* first_drop = c->cmp_off + n + 1;
+    uint64_t* info_dev = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(c->dec_hint_dev) + 64);
+    volatile uint64_t* info = reinterpret_cast<volatile uint64_t*>(reinterpret_cast<uint8_t*>(c->dec_hint_host) + 64);
+    e = hipMemsetAsync(first_drop, 0xFF, sizeof(uint64_t), c->stream);
+    if (e != hipSuccess) return fail(c, e, "hipMemsetAsync");
+    rc = run(c, ONC_K_COMPACT, "compact_lens",
+             [&] { return onc::launch_compact_lens(rec_off, status, n, c->lens, first_drop, c->stream); });
+    if (rc == ONC_RC_OK) rc = onc_scan_lengths(c, c->lens, n, 0, c->cmp_off);
+    if (rc == ONC_RC_OK)
+        rc = run(c, ONC_K_COMPACT, "compact_info",
+                 [&] { return onc::launch_compact_info(rec_off, c->cmp_off, n, first_drop, info_dev, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return fail(c, e, "hipStreamSynchronize");
+    const uint64_t fb = info[0], base = info[1], lo = info[2], new_end = info[4];
+    if (total) *total = fb < n ? new_end : info[3];
+    if (fb >= n) return ONC_RC_OK;                       // no extent to drop: nothing moves
+    const uint64_t moved = new_end - lo;
+    if (moved) {
+        rc = ensure_buf(c, c->cmp_bytes, c->cmp_bytes_cap, moved + 16, "hipMalloc(compact bytes)");
+        if (rc != ONC_RC_OK) return rc;
+        rc = run(c, ONC_K_COMPACT, "compact_gather", [&] {
+            return onc::launch_compact_gather(out, rec_off, c->cmp_off, fb, n, base, lo, c->cmp_bytes, c->stream);
+        });
+        if (rc != ONC_RC_OK) return rc;
+        e = hipMemcpyAsync(out + lo, c->cmp_bytes, moved, hipMemcpyDefault, c->stream);   // (out may be mapped host memory)
+        if (e != hipSuccess) return fail(c, e, "hipMemcpyAsync");
+    }
+    return run(c, ONC_K_COMPACT, "compact_offsets",
+               [&] { return onc::launch_compact_offsets(rec_off, c->cmp_off, fb, n, base, c->stream); });
+}
+
+int onc_compact_iov(onc_codec* c, onc_iov_rec* iov, const int32_t* status, uint64_t n, uint64_t* totals) {
+    if (!c || (n && (!iov || !status))) return ONC_RC_EINVAL;
+    if (set_device(c) != ONC_RC_OK) return ONC_RC_EHIP;
+    hipError_t e;
+    if (totals) {
+        e = hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), c->stream);
+        if (e != hipSuccess) return fail(c, e, "hipMemsetAsync");
+    }
+    if (n == 0) return ONC_RC_OK;
+    int rc = ensure_lens(c, n);
+    if (rc == ONC_RC_OK) rc = ensure_buf(c, c->cmp_off, c->cmp_off_cap, n + 2, "hipMalloc(compact offsets)");
+    if (rc != ONC_RC_OK) return rc;
+    forget_plan(c);
+    rc = run(c, ONC_K_COMPACT, "compact_iov_lens",
+             [&] { return onc::launch_compact_iov_lens(iov, status, n, c->lens, c->stream); });
+    if (rc == ONC_RC_OK) rc = onc_scan_lengths(c, c->lens, n, 0, c->cmp_off);
+    if (rc != ONC_RC_OK) return rc;
+    return run(c, ONC_K_COMPACT, "compact_iov_apply",
+               [&] { return onc::launch_compact_iov_apply(iov, status, n, c->cmp_off, totals, c->stream); });
 }
 
 int32_t onc_expected_message_len(const uint8_t* data, uint64_t len, uint32_t* out) {

@@ -516,8 +516,7 @@ static_assert(kDecTile == 64, "kFromLen: one wave per workgroup, 64 workgroup to
 // (kLine1Min, kernels.h; break-even measured at ~1/3) — no policy code in
 // either kernel. A device-memory word read by every workgroup cost the c1
 // decode 1-2 us of prologue; results never depend on the policy (only which
-// chunks each round loads); variant bits 0x80000 / 0x100000 force the line /
-// the standard policy (tests).
+// chunks each round loads); onc_codec_set_decode_policy pins either (tests).
 
 // The window of one record (L != 0): round 1, the header extent, round 2.
 // Returns the chunks staged in LDS; needs2: the header reaches past the
@@ -746,12 +745,8 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
         if (kRoot && a.consumed) a.consumed[i] = st == ONC_OK ? consumed : 0u;
         if (kNTOut) {
             __builtin_nontemporal_store(st, a.out.status + i);
-            // (lab, ONC_VARIANT_DEC_AUX_SPARSE: aux words only for failing
-            // records — 8 of the 76 bytes written per OK record)
-            if (!(a.variant & ONC_VARIANT_DEC_AUX_SPARSE) || st != ONC_OK) {
-                __builtin_nontemporal_store(aux0, a.out.aux0 + i);
-                __builtin_nontemporal_store(aux1, a.out.aux1 + i);
-            }
+            __builtin_nontemporal_store(aux0, a.out.aux0 + i);
+            __builtin_nontemporal_store(aux1, a.out.aux1 + i);
         } else {
             a.out.status[i] = st;
             a.out.aux0[i] = aux0;

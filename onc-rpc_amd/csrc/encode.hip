@@ -581,123 +581,54 @@ __device__ __forceinline__ void img_placeholder(uint32_t* img32, ImgSink& w, uin
     w.prev = 0u;
 }
 
-// Single pass (ONC_VARIANT_SINGLE_PASS, lab): the tile's place without an
-// enc_len launch. Tiles are claimed in start order (enc_emit_kernel_t), so a
-// wave only ever waits on tiles claimed earlier by waves that are running or
-// done — no deadlock when the grid is not fully resident. The wave publishes
-// its tile's total, sums the totals of its predecessors from the nearest one
-// that has published its inclusive prefix (256 states per round, one load
-// per lane per 64), and publishes its own prefix. A wave that finds a
-// predecessor not yet published re-reads; past kLbSpinLimit rounds it gives
-// up and flags lb_fail (a bound, never a hang).
-constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
-constexpr uint32_t kLbSpinLimit = 1u << 16;
-#ifndef ONC_LB_W
-#define ONC_LB_W 1
-#endif
-#ifndef ONC_LB_W0
-#define ONC_LB_W0 1
-#endif
-constexpr int kLbW = ONC_LB_W;                    // states per lane per round (64 * kLbW per round)
-constexpr int kLbW0 = ONC_LB_W0;                  // the first round's (the nearest predecessors)
-__device__ __forceinline__ uint64_t tile_lookback(const EncArgs& a, uint64_t t, uint64_t agg) {
-    const int lane = threadIdx.x & 63;
-    if (lane == 0) __hip_atomic_store(a.lb_state + t, kLbAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t excl = 0;
-    int64_t j = int64_t(t);                        // tiles [0, j) not summed yet
-    uint32_t spins = 0;
-    int w = kLbW0;
-    while (j > 0) {
-        uint64_t v[kLbW];
-#pragma unroll
-        for (int k = 0; k < kLbW; ++k) {
-            const int64_t idx = j - 1 - lane - 64 * k;
-            v[k] = idx >= 0 && k < w ? __hip_atomic_load(a.lb_state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                     : kLbIncl;
-        }
-        bool done = false, retry = false;
-        uint64_t sum = 0;
-#pragma unroll
-        for (int k = 0; k < kLbW; ++k) {
-            if (done || retry || k >= w) continue;
-            const uint64_t incl = __ballot((v[k] >> 62) == 2);
-            const uint64_t empty = __ballot((v[k] >> 62) == 0);
-            const int first = incl ? __builtin_ctzll(incl) : 64;
-            const uint64_t upto = first == 64 ? ~0ull : ((2ull << first) - 1);     // lanes <= first
-            if (empty & upto) {
-                retry = true;
-            } else {
-                sum += lane_u64(wave_incl_scan_u64(uint64_t(lane) <= uint64_t(first) ? (v[k] & kLbVal) : 0), 63);
-                done = first < 64;
-            }
-        }
-        if (retry) {
-            if (++spins > kLbSpinLimit) {
-                if (lane == 0) atomicOr(a.lb_fail, 1u);
-                break;
-            }
-            continue;                               // this round's sums dropped: read it again
-        }
-        excl += sum;
-        if (done) break;
-        j -= 64 * w;
-        w = kLbW;
-    }
-    if (lane == 0) __hip_atomic_store(a.lb_state + t, kLbIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return excl;
-}
-
-// ONC_VARIANT_SP_WG_LOOKBACK (lab, with a workgroup claim or blockIdx
-// order): one look-back per workgroup over workgroup states instead of one
-// per tile — a quarter of the states, read by a quarter of the waves. The
-// waves of the workgroup hand their tile totals to wave 0 through LDS
-// flags (waves whose tile lies past the batch do not take part), wave 0
-// looks back for the workgroup and hands the base back.
+// The one-launch small batch (codec.hip small_batch: at most kSpWaves tiles,
+// so the one workgroup of enc_emit_single_kernel is the whole batch): each
+// wave plans its tile, hands the tile's byte total to wave 0 through LDS,
+// and wave 0 hands back the exclusive prefix of the totals. All waves of a
+// workgroup are resident together, so waiting on a flag another wave of it
+// sets always ends; there is no predecessor workgroup and nothing in global
+// memory to wait on. (Rounds 5's single-pass lab placed the tiles of larger
+// batches by a decoupled look-back across workgroups; measured slower than
+// enc_len + enc_emit and removed — DESIGN.md §4, profiles/HISTORY.md.)
 template <int kGW>
-struct WgLbT {
+struct WgPlace {
     uint64_t agg[kGW];
-    uint64_t base;
-    uint32_t ready[kGW];            // wave w's total is in agg[w] (w > 0); ready[0]: base is set
+    uint64_t base[kGW];
+    uint32_t ready[kGW];            // wave w's total is in agg[w] (w > 0); ready[0]: the bases are set
 };
-using WgLb = WgLbT<kFastWaves>;
 __device__ __forceinline__ uint32_t lds_flag(const uint32_t* f) {
     return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 template <int kGW>
-__device__ __forceinline__ uint64_t wg_lookback(const EncArgs& a, WgLbT<kGW>& X, uint64_t tile, uint64_t agg) {
+__device__ __forceinline__ uint64_t wg_place(WgPlace<kGW>& X, uint64_t tile, uint64_t agg, uint64_t ntiles) {
     const int lane = threadIdx.x & 63;
     const int w = int(tile % kGW);
-    const uint64_t g = tile / kGW;
-    const uint64_t ntiles = num_emit_tiles(a.n);
-    const int live = int(min(uint64_t(kGW), ntiles - g * kGW));
+    const int live = int(min(uint64_t(kGW), ntiles - tile / kGW * kGW));
     if (w != 0) {
         if (lane == 0) {
             X.agg[w] = agg;
             __hip_atomic_store(&X.ready[w], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         while (__builtin_amdgcn_readfirstlane(int(lds_flag(&X.ready[0]))) == 0) __builtin_amdgcn_s_sleep(1);
-    } else {
-        uint64_t total = agg;
-        for (int v = 1; v < live; ++v) {
-            while (__builtin_amdgcn_readfirstlane(int(lds_flag(&X.ready[v]))) == 0) __builtin_amdgcn_s_sleep(1);
-            total += X.agg[v];
-        }
-        const uint64_t excl = tile_lookback(a, g, total);
-        if (lane == 0) {
-            X.agg[0] = agg;
-            X.base = excl;
-            __hip_atomic_store(&X.ready[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        return X.base[w];
     }
-    uint64_t b = X.base;
-    for (int v = 0; v < w; ++v) b += X.agg[v];
-    return b;
+    uint64_t run = agg;
+    for (int v = 1; v < live; ++v) {
+        while (__builtin_amdgcn_readfirstlane(int(lds_flag(&X.ready[v]))) == 0) __builtin_amdgcn_s_sleep(1);
+        if (lane == 0) X.base[v] = run;
+        run += X.agg[v];
+    }
+    if (lane == 0) __hip_atomic_store(&X.ready[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return 0;
 }
 
-template <int kU, int kNT, bool kFused, bool kRoot = false, bool kGiven = false, bool kPre = false,
-          bool kLen = false, bool kSingle = false, int kGW = kFastWaves>
+// kSmall: the tile of a one-workgroup small batch (enc_emit_single_kernel):
+// planned here (enc_len's plan, statuses and lengths written) and placed
+// through X (wg_place) instead of by enc_len's totals.
+template <int kU, int kNT, bool kFused, bool kRoot = false, bool kGiven = false, bool kLen = false,
+          bool kSmall = false, int kGW = kFastWaves>
 __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint64_t tile, uint64_t given = 0,
-                                              WgLbT<kGW>* X = nullptr) {
+                                              WgPlace<kGW>* X = nullptr) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = tile * kEmitRecs;
     uint32_t* img32 = reinterpret_cast<uint32_t*>(T.img);
@@ -708,12 +639,12 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     // together, one memory round trip before the planning starts.
     ONC_PROF(0);
     TileLoads<kFused> tl;
-    if constexpr (!kSingle) tl = tile_loads<kFused, kGiven>(a, tile, given);
+    if constexpr (!kSmall) tl = tile_loads<kFused, kGiven>(a, tile, given);
     MsgRegs mr = issue_msg(a.msgs + r0 + min(lane, nrec - 1));
     // kLen: the plan's length of the lane's record, issued with the rest
     uint32_t glen = 0;
     if constexpr (kLen) glen = a.len_in[r0 + min(lane, nrec - 1)];
-    if constexpr (kSingle) {
+    if constexpr (kSmall) {
         asm volatile("" : "+v"(mr.q[0]), "+v"(mr.q[1]), "+v"(mr.q[2]), "+v"(mr.q[3]));
     } else if constexpr (kFused) {
         static_assert(TileLoads<kFused>::kW == 16, "pin list below");
@@ -729,18 +660,11 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     // output coordinates: byte 0 = the 16-aligned chunk base below the
     // caller's `out`, which sits at `origin` (any writer position)
     uint64_t T0 = 0;
-    if constexpr (!kSingle) T0 = a.origin + (kGiven ? 0ull : launch_base(a)) + tile_reduce<kFused>(tl, tile);
+    if constexpr (!kSmall) T0 = a.origin + (kGiven ? 0ull : launch_base(a)) + tile_reduce<kFused>(tl, tile);
     ONC_PROF(1);
     uint64_t len = 0, poff = 0;
     uint32_t hw = 0;
     bool word_aligned = true;
-    // kPre (lab, ONC_VARIANT_EMIT_PRELOAD): a Call's AUTH_UNIX credential
-    // block issued with the header build's descriptor reload (one round trip,
-    // not two dependent; round 3: c0 enc_emit 105 -> 102.5 us). With the
-    // declared-length checks it spills 4 VGPRs inside the gid writes (each
-    // reload a vmcnt(0) wait): c0 enc_emit 117 us against 98 without it.
-    const bool cred_unix = kPre && !kRoot && dm.msg_type == ONC_MSG_CALL && (dm.cred.kind_len >> 24) == ONC_KIND_UNIX;
-    const uint64_t cred_ref = dm.cred.ref;
     if (lane < nrec) {
         const onc_msg& d = dm;
         if constexpr (kLen) {
@@ -751,7 +675,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                               (d.msg_type == ONC_MSG_REPLY && d.reply_stat == ONC_REPLY_ACCEPTED &&
                                d.stat == ONC_ACCEPT_SUCCESS);
             hw = len ? uint32_t((len - (body ? uint64_t(d.payload_len) : 0ull)) >> 2) : 0;
-        } else if constexpr (kSingle) {
+        } else if constexpr (kSmall) {
             // enc_len's plan of the record (its decl 1 form) and its outputs
             RecPlan p = plan_record<true>(d, a.unix, a.bounds);
             if (p.status != ONC_OK) p = plan_record<false>(d, a.unix, a.bounds);
@@ -770,8 +694,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         word_aligned = (len & 3) == 0 && (len == 4ull * hw || ((payload + d.payload_off) & 3) == 0);
     }
     const uint64_t incl = wave_incl_scan_u64(len);
-    if constexpr (kSingle)
-        T0 = a.origin + launch_base(a) + (X ? wg_lookback(a, *X, tile, lane_u64(incl, 63)) : tile_lookback(a, tile, lane_u64(incl, 63)));
+    if constexpr (kSmall) T0 = a.origin + wg_place(*X, tile, lane_u64(incl, 63), num_emit_tiles(a.n));
     const uint64_t start = T0 + incl - len;
     const uint64_t en = start + len;
     const uint64_t pst = start + 4ull * hw;
@@ -841,12 +764,6 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                 // reloaded (an L2 hit) rather than kept live across the span
                 // loop (kept live: 162 VGPRs, 3 waves per SIMD)
                 MsgRegs mr2 = issue_msg(a.msgs + r0 + lane);
-                UnixRegs cq;
-                if (cred_unix) {
-                    cq = issue_unix(a.unix, cred_ref);    // validated by plan_record (len != 0)
-                    asm volatile("" : "+v"(cq.q[0]), "+v"(cq.q[1]), "+v"(cq.q[2]), "+v"(cq.q[3]), "+v"(cq.q[4]),
-                                 "+v"(cq.q[5]));
-                }
                 asm volatile("" : "+v"(mr2.q[0]), "+v"(mr2.q[1]), "+v"(mr2.q[2]), "+v"(mr2.q[3]));
                 const onc_msg d = as_msg(mr2);
                 const EncSrc src{a.unix, reinterpret_cast<uintptr_t>(a.auth_arena), payload};
@@ -861,7 +778,7 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                 // nothing extra live across the header build)
                 DeclCheck dc{a.bounds.auth_len, &T.bad[lane]};
                 if (kRoot) put_root_words(d, uint32_t(len), src, a.root, w);
-                else put_header_words(d, uint32_t(len), src, w, &cq, cred_unix, &dc);
+                else put_header_words(d, uint32_t(len), src, w, nullptr, false, &dc);
                 if (!kRoot) {
                     const int32_t bad = T.bad[lane];
                     if (bad != ONC_OK) {
@@ -1375,57 +1292,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
 // kernel boundary). The message instances need 106 VGPRs (4 waves per SIMD;
 // held there by the attribute); squeezed to 5 waves per SIMD (96 VGPRs) they
 // spill. The body-root instances keep what they need (140 VGPRs).
-template <int kU, int kNT = 0, bool kFused = false, bool kRoot = false, bool kLen = false, bool kPre = false,
-          bool kSingle = false>
+template <int kU, int kNT = 0, bool kFused = false, bool kRoot = false, bool kLen = false>
 __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(kRoot ? 1 : 4))) void enc_emit_kernel_t(EncArgs a) {
     __shared__ ImgTile s_tiles[kFastWaves];
-    uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
-    if constexpr (kSingle) {
-        // tiles claimed in start order (the claim counter is the word after
-        // the tiles' states): one claim per wave, or (ONC_VARIANT_SP_WG_CLAIM)
-        // one per workgroup for its kFastWaves tiles, or (ONC_VARIANT_SP_BLOCK_ORDER)
-        // none — blockIdx order, which waits only on earlier workgroups if the
-        // dispatcher starts them in order (lab)
-        uint32_t* ctr = reinterpret_cast<uint32_t*>(a.lb_state + num_emit_tiles(a.n));
-        __shared__ WgLb s_lb;
-        const bool wgl = (a.variant & ONC_VARIANT_SP_WG_LOOKBACK) &&
-                         (a.variant & (ONC_VARIANT_SP_WG_CLAIM | ONC_VARIANT_SP_BLOCK_ORDER));
-        if (wgl) {
-            if (threadIdx.x < kFastWaves) s_lb.ready[threadIdx.x] = 0u;
-            __syncthreads();                        // every wave of the workgroup is here
-        }
-        if (a.variant & ONC_VARIANT_SP_WG_CLAIM) {
-            __shared__ uint32_t s_claim;
-            if (threadIdx.x == 0) s_claim = atomicAdd(ctr, 1u);
-            __syncthreads();
-            tile = uint64_t(s_claim) * kFastWaves + (threadIdx.x >> 6);
-        } else if (!(a.variant & ONC_VARIANT_SP_BLOCK_ORDER)) {
-            uint32_t t = 0;
-            if ((threadIdx.x & 63) == 0) t = atomicAdd(ctr, 1u);
-            tile = uint32_t(__builtin_amdgcn_readfirstlane(int(t)));
-        }
-        if (tile < num_emit_tiles(a.n))
-            enc_emit_tile<kU, kNT, kFused, kRoot, false, kPre, kLen, kSingle>(a, s_tiles[threadIdx.x >> 6], tile, 0,
-                                                                              wgl ? &s_lb : nullptr);
-        return;
-    }
+    const uint64_t tile = uint64_t(blockIdx.x) * kFastWaves + (threadIdx.x >> 6);
     if (tile < num_emit_tiles(a.n))
-        enc_emit_tile<kU, kNT, kFused, kRoot, false, kPre, kLen, kSingle>(a, s_tiles[threadIdx.x >> 6], tile);
+        enc_emit_tile<kU, kNT, kFused, kRoot, false, kLen>(a, s_tiles[threadIdx.x >> 6], tile);
 }
 
-// Single pass with kSpWaves tiles per workgroup (ONC_VARIANT_SP_WG8, lab):
-// blockIdx order and one look-back per workgroup, over half the states the
-// 4-wave workgroups publish (8 image tiles: 2 workgroups per CU by LDS, the
-// same 4 waves per SIMD).
+// The one-launch small batch (codec.hip small_batch): one workgroup of
+// kSpWaves tile waves is the whole batch (8 image tiles: the same 4 waves per
+// SIMD as the 4-wave kernel).
 __global__ __launch_bounds__(64 * kSpWaves) __attribute__((amdgpu_waves_per_eu(4))) void enc_emit_single_kernel(EncArgs a) {
     __shared__ ImgTile s_tiles[kSpWaves];
-    __shared__ WgLbT<kSpWaves> s_lb;
-    if (threadIdx.x < kSpWaves) s_lb.ready[threadIdx.x] = 0u;
+    __shared__ WgPlace<kSpWaves> s_place;
+    if (threadIdx.x < kSpWaves) s_place.ready[threadIdx.x] = 0u;
     __syncthreads();
-    const uint64_t tile = uint64_t(blockIdx.x) * kSpWaves + (threadIdx.x >> 6);
+    const uint64_t tile = uint64_t(threadIdx.x >> 6);
     if (tile < num_emit_tiles(a.n))
-        enc_emit_tile<kEmitChunkUnroll, kEmitNT, false, false, false, false, false, true, kSpWaves>(
-            a, s_tiles[threadIdx.x >> 6], tile, 0, &s_lb);
+        enc_emit_tile<kEmitChunkUnroll, kEmitNT, false, false, false, false, true, kSpWaves>(
+            a, s_tiles[threadIdx.x >> 6], tile, 0, &s_place);
 }
 
 hipError_t launch_enc_len(const EncArgs& a, hipStream_t s) {
@@ -1463,23 +1349,9 @@ hipError_t launch_enc_emit(const EncArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     const dim3 g{uint32_t(blocks)}, b{uint32_t(64 * kFastWaves)};
-    if (a.lb_state && (a.variant & ONC_VARIANT_SP_WG8)) {
-        ONC_LAUNCH(enc_emit_single_kernel, dim3(uint32_t((num_emit_tiles(a.n) + kSpWaves - 1) / kSpWaves)),
-                   dim3(64 * kSpWaves), 0, s, a);
-        return hipGetLastError();
-    }
-    if (a.lb_state) {                               // (lab: the single pass, codec.hip single_pass)
-        ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false, false, false, false, true>), g, b, 0, s, a);
-        return hipGetLastError();
-    }
-    if (a.variant & ONC_VARIANT_EMIT_PRELOAD) {     // (lab: the round-3 credential-block preload)
-        if (a.len_in) {
-            if (a.fused_base) ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, true, false, true, true>), g, b, 0, s, a);
-            else ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false, false, true, true>), g, b, 0, s, a);
-        } else {
-            if (a.fused_base) ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, true, false, false, true>), g, b, 0, s, a);
-            else ONC_LAUNCH((enc_emit_kernel_t<kEmitChunkUnroll, kEmitNT, false, false, false, true>), g, b, 0, s, a);
-        }
+    if (a.small) {
+        if (num_emit_tiles(a.n) > uint64_t(kSpWaves)) return hipErrorInvalidValue;   // one workgroup is the batch
+        ONC_LAUNCH(enc_emit_single_kernel, dim3(1), dim3(64 * kSpWaves), 0, s, a);
         return hipGetLastError();
     }
     if (a.len_in) {

@@ -63,12 +63,8 @@ struct EncArgs {
     const uint64_t* base_dev;   // optional: output bytes before this launch's first record (chunked encode)
     const uint32_t* len_in;     // optional (wave-per-tile enc_emit): the plan's record lengths, read instead
                                 // of re-planning (no dependent AUTH_UNIX parameter load in the prologue)
-    // single pass (ONC_VARIANT_SINGLE_PASS, lab): no enc_len launch; every emit wave claims a tile id in
-    // start order, plans it and places it by a decoupled look-back over these words (zeroed before the
-    // launch): lb_state[tile] = flag << 62 | bytes (1: the tile's own total, 2: the inclusive prefix);
-    // lb_state[ntiles] = the claim counter
-    uint64_t* lb_state;
-    uint32_t* lb_fail;          // set when a look-back gave up (a bound on its spins: never a hang)
+    uint32_t small;             // the one-launch small batch (enc_emit_single_kernel: one workgroup, the
+                                // tiles planned and placed inside it; <= kSpWaves tiles)
 #ifdef ONC_EMIT_PROF
     uint64_t* prof;         // lab builds only (tools/emit_prof.hip): per-tile phase timestamps
 #endif
@@ -183,6 +179,19 @@ hipError_t launch_store_u64(uint64_t* p, uint64_t v, hipStream_t s);
 hipError_t launch_lenblk(const uint32_t* len, uint64_t n, uint64_t* blk_sum, hipStream_t s);
 hipError_t launch_lenoff(const uint32_t* len, uint64_t n, const uint64_t* blk_sum, uint64_t base, uint64_t* rec_off,
                          hipStream_t s);
+// compact.hip
+hipError_t launch_compact_lens(const uint64_t* rec_off, const int32_t* status, uint64_t n, uint32_t* lens,
+                               uint64_t* first_drop, hipStream_t s);
+hipError_t launch_compact_info(const uint64_t* rec_off, const uint64_t* new_off, uint64_t n,
+                               const uint64_t* first_drop, uint64_t* info, hipStream_t s);
+hipError_t launch_compact_gather(const uint8_t* out, const uint64_t* rec_off, const uint64_t* new_off, uint64_t fb,
+                                 uint64_t n, uint64_t base, uint64_t lo, uint8_t* scratch, hipStream_t s);
+hipError_t launch_compact_offsets(uint64_t* rec_off, const uint64_t* new_off, uint64_t fb, uint64_t n, uint64_t base,
+                                  hipStream_t s);
+hipError_t launch_compact_iov_lens(const onc_iov_rec* iov, const int32_t* status, uint64_t n, uint32_t* lens,
+                                   hipStream_t s);
+hipError_t launch_compact_iov_apply(onc_iov_rec* iov, const int32_t* status, uint64_t n, const uint64_t* new_off,
+                                    uint64_t* totals, hipStream_t s);
 // decode.hip
 hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s);
 hipError_t launch_dlen_tiles(const uint32_t* rec_len, uint64_t n, uint64_t* tile_sum, uint64_t* blk_sum, hipStream_t s);
@@ -190,9 +199,8 @@ hipError_t launch_dlen_tiles(const uint32_t* rec_len, uint64_t n, uint64_t* tile
 __host__ __device__ inline uint64_t num_tiles(uint64_t n) { return (n + 255) / 256; }
 __host__ __device__ inline uint64_t num_len_blocks(uint64_t n) { return (n + kLenRecs - 1) / kLenRecs; }
 __host__ __device__ inline uint64_t num_emit_tiles(uint64_t n) { return (n + kEmitRecs - 1) / kEmitRecs; }
-// enc_emit_single_kernel: tiles (waves) per workgroup — the single pass's
-// look-back granule, and the size of the one-launch small-batch encode
-// (kSpWaves * kEmitRecs records: one workgroup, nothing to look back over)
+// enc_emit_single_kernel: tiles (waves) of its one workgroup — the largest
+// one-launch small-batch encode is kSpWaves * kEmitRecs records
 #ifndef ONC_SP_WAVES
 #define ONC_SP_WAVES 8
 #endif

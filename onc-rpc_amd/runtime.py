@@ -21,10 +21,10 @@ LIB_PATH = os.environ.get("ONC_RPC_AMD_LIB") or os.path.join(os.path.dirname(os.
 K_NAMES = ["enc_len_kernel", "scan_tiles_kernel", "enc_emit_kernel", "decode_kernel",
            "len_tiles_kernel", "len_apply_kernel", "iov_len_kernel", "iov_emit_kernel",
            "frame_chunks_kernel", "frame_write_kernel", "frame_walk_kernel",
-           "frame_counts_kernel", "frame_guess_kernel"]
+           "frame_counts_kernel", "frame_guess_kernel", "compact_kernels"]
 (K_ENC_LEN, K_SCAN_TILES, K_ENC_EMIT, K_DEC_PARSE, K_LEN_TILES, K_LEN_APPLY, K_IOV_LEN,
- K_IOV_EMIT, K_FRAME, K_FRAME_WRITE, K_FRAME_WALK, K_FRAME_COUNTS, K_FRAME_GUESS) = range(13)
-ABI_VERSION = 7
+ K_IOV_EMIT, K_FRAME, K_FRAME_WRITE, K_FRAME_WALK, K_FRAME_COUNTS, K_FRAME_GUESS, K_COMPACT) = range(14)
+ABI_VERSION = 8
 K_COUNT = len(K_NAMES)
 
 # every symbol include/onc_rpc.h declares
@@ -36,6 +36,7 @@ EXPORTED = [
     "onc_expected_message_len", "onc_encode_iov", "onc_frame_stream", "onc_encode_plan", "onc_encode_emit",
     "onc_decode_lengths", "onc_decode_body", "onc_encode_body", "onc_encode_body_lengths",
     "onc_codec_create_ex", "onc_codec_set_decode_policy", "onc_host_register", "onc_host_unregister",
+    "onc_compact", "onc_compact_iov",
 ]
 
 # onc_codec_options (include/onc_rpc.h)
@@ -43,10 +44,7 @@ DECODE_POLICY_AUTO, DECODE_POLICY_STANDARD, DECODE_POLICY_LINE = 0, 1, 2
 OPT_FORCE_SCAN = 0x1
 VARIANT_EMIT_WS, VARIANT_EMIT_TILE = 0x200, 0x400
 VARIANT_WS_NO_INTERIOR, VARIANT_WS_NO_FULL, VARIANT_WS_PIPELINE = 0x4000, 0x8000, 0x10000
-VARIANT_EMIT_REPLAN, VARIANT_WHOLE_PLAN, VARIANT_EMIT_PRELOAD = 0x20000, 0x40000, 0x80000
-VARIANT_SINGLE_PASS = 0x200000
-VARIANT_SP_WG_CLAIM, VARIANT_SP_BLOCK_ORDER, VARIANT_SP_WG_LOOKBACK = 0x400000, 0x800000, 0x1000000
-VARIANT_SP_WG8 = 0x2000000
+VARIANT_EMIT_REPLAN, VARIANT_WHOLE_PLAN = 0x20000, 0x40000
 # options every Codec() gets unless it is given its own (bench.py --variant)
 DEFAULT_OPTIONS: dict = {}
 
@@ -113,6 +111,8 @@ def load_library(path=LIB_PATH):
     lib.onc_encode_body_lengths.argtypes = [vp, i32, C.POINTER(OncBatch), vp, vp]
     lib.onc_host_register.argtypes = [vp, vp, u64, C.POINTER(vp)]
     lib.onc_host_unregister.argtypes = [vp, vp]
+    lib.onc_compact.argtypes = [vp, vp, vp, vp, u64, C.POINTER(C.c_uint64)]
+    lib.onc_compact_iov.argtypes = [vp, vp, vp, u64, vp]
     for name in EXPORTED:
         getattr(lib, name).restype = getattr(lib, name).restype or i32
     # a stale library would read a differently laid out onc_batch and label
@@ -323,6 +323,19 @@ class Codec:
         self._check(self.lib.onc_encode_body(self.h, root, C.byref(b), _ptr(out), cap, _ptr(rec_off), _ptr(status),
                                              _ptr(rec_len)), "onc_encode_body")
 
+    def compact(self, out, rec_off, status, n):
+        """onc_compact: the extents of records with status != OK dropped from
+        an encoded buffer in place (rec_off rewritten); returns the new
+        rec_off[n]."""
+        total = C.c_uint64(0)
+        self._check(self.lib.onc_compact(self.h, _ptr(out), _ptr(rec_off), _ptr(status), n, C.byref(total)),
+                    "onc_compact")
+        return total.value
+
+    def compact_iov(self, iov, status, n, totals=None):
+        """onc_compact_iov: failing records' iovecs emptied, wire_off re-placed."""
+        self._check(self.lib.onc_compact_iov(self.h, _ptr(iov), _ptr(status), n, _ptr(totals)), "onc_compact_iov")
+
     def scan_lengths(self, rec_len, n, base, rec_off):
         self._check(self.lib.onc_scan_lengths(self.h, _ptr(rec_len), n, base, _ptr(rec_off)),
                     "onc_scan_lengths")
@@ -367,8 +380,11 @@ class HostMapped:
         return self.host.view(dtype)
 
     def close(self):
-        if self._dev is not None and self._codec.h:
-            self._codec.lib.onc_host_unregister(self._codec.h, C.c_void_p(self._addr))
+        # unregistered whether or not its codec is still open (a pinned range
+        # belongs to the process: onc_host_unregister takes a NULL codec), so
+        # the pages are unpinned before the mapping is freed
+        if self._dev is not None:
+            self._codec.lib.onc_host_unregister(self._codec.h or None, C.c_void_p(self._addr))
         self._dev = None
 
     def __del__(self):

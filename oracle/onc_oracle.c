@@ -1100,6 +1100,25 @@ void oracle_decode_batch_mt(const uint8_t* wire, const uint64_t* rec_off, uint64
  * record boundary (or max_records were framed), else the expected_message_len
  * error or IncompleteMessage{remaining bytes, wanted} for a record that runs
  * past the end. */
+/* serialise_into writes nothing for a message that fails: its panics fire
+ * before the first write (flavor.rs:110 assert!, unix_params.rs:47 / :149
+ * in the constructors) and the length check returns before it
+ * (rpc_message.rs:146-151). A batch output restated as that loop's buffer:
+ * the OK records' bytes, in order, from rec_off[0] on (memmove: every record
+ * moves toward the start). */
+uint64_t oracle_compact(uint8_t* wire, uint64_t* rec_off, const int32_t* status, uint64_t n) {
+    uint64_t w = n ? rec_off[0] : 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t a = rec_off[i], len = rec_off[i + 1] - a;
+        rec_off[i] = w;
+        if (status[i] != ONC_OK) continue;
+        if (w != a) memmove(wire + w, wire + a, len);
+        w += len;
+    }
+    if (n) rec_off[n] = w;
+    return w;
+}
+
 void oracle_frame_stream(const uint8_t* data, uint64_t len, uint64_t* rec_off, uint64_t max_records,
                          uint64_t* result) {
     uint64_t pos = 0, n = 0;

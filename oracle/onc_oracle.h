@@ -71,6 +71,12 @@ void oracle_encode_batch_mt(uint64_t n, const onc_msg* msgs, const onc_unix_para
 void oracle_frame_stream(const uint8_t* data, uint64_t len, uint64_t* rec_off, uint64_t max_records,
                          uint64_t* result);
 
+/* The bytes a loop of serialise_into calls on one Cursor<Vec<u8>> leaves
+ * when some messages fail (a failing message writes nothing): the extents of
+ * records with status != OK dropped from an encoded buffer in place, rec_off
+ * re-placed (onc_compact). Returns the new rec_off[n]. */
+uint64_t oracle_compact(uint8_t* wire, uint64_t* rec_off, const int32_t* status, uint64_t n);
+
 /* Component-level entry points used by the golden-vector tests. */
 /* expected_message_len — src/rpc_message.rs:343-367 */
 int32_t oracle_expected_message_len(const uint8_t* data, uint64_t len, uint32_t* out);

@@ -47,6 +47,8 @@ def load():
     lib.oracle_encode_batch_mt.argtypes = [u64, vp, vp, vp, vp, vp, vp, vp, vp, i32]
     lib.oracle_encode_batch_mt.restype = None
     lib.oracle_frame_stream.argtypes = [vp, u64, vp, u64, vp]
+    lib.oracle_compact.argtypes = [vp, vp, vp, u64]
+    lib.oracle_compact.restype = u64
     lib.oracle_frame_stream.restype = None
     lib.oracle_expected_message_len.argtypes = [vp, u64, vp]
     lib.oracle_expected_message_len.restype = C.c_int32
@@ -156,6 +158,16 @@ def frame_stream(buf, max_records=None):
     lib.oracle_frame_stream(_p(a), len(buf), _p(off), n_max, _p(res))
     n = int(res[0])
     return off[:n + 1], n, int(res[1]), int(np.int64(res[2])), int(res[3]), int(res[4])
+
+
+def compact(wire, rec_off, status):
+    """oracle_compact of an encoded batch -> (bytes, rec_off u64[n+1])."""
+    lib = load()
+    a = np.frombuffer(bytes(wire), np.uint8).copy()
+    off = np.asarray(rec_off, np.uint64).copy()
+    st = np.ascontiguousarray(status, np.int32)
+    total = lib.oracle_compact(_p(a), _p(off), _p(st), len(st))
+    return a[:total].tobytes(), off
 
 
 def decode_message(buf: bytes, mode):

@@ -387,6 +387,28 @@ static void test_stream_framing(Codec& c) {
     CHECK(stop->buffer_len() == a.size() - 10 && stop->expected() == a.size());
 }
 
+// A 16 MiB socket buffer framed and decoded by a fresh codec: the stage holds
+// the wire and the offsets while framing, and the decode outputs only for the
+// records framed (it grows keeping the staged wire; sized for every possible
+// 4-byte record the outputs alone would be ~1.1 GB of pinned memory).
+static void test_stream_stage_size(Codec&) {
+    Codec c(0);
+    const std::vector<uint8_t> a = fixture("call_auth_unix_16gids_288B");
+    std::vector<uint8_t> stream;
+    while (stream.size() + a.size() <= (size_t(16) << 20)) stream.insert(stream.end(), a.begin(), a.end());
+    const size_t n = stream.size() / a.size();
+    BatchDecoder dec;
+    size_t consumed = 0;
+    std::optional<Error> stop;
+    const std::vector<Decoded> out = dec.try_from_stream(c, stream.data(), stream.size(), DecodeMode::Slice,
+                                                         &consumed, &stop);
+    CHECK(out.size() == n && consumed == stream.size() && !stop.has_value());
+    for (size_t i = 0; i < n; i += 997) CHECK(out[i].ok() && out[i].message->xid() == 643743997u);
+    CHECK(out[n - 1].ok());
+    std::printf("  stream of %zu bytes (%zu records): stage %zu MiB\n", stream.size(), n, c.stage_capacity() >> 20);
+    CHECK(c.stage_capacity() <= (size_t(128) << 20));
+}
+
 // ---- body-level types (onc_decode_body / onc_encode_body) -----------------------
 
 // flavor.rs:232-266 test_auth_unix_unaligned_machinename, :268-320 test_auth_unix
@@ -544,6 +566,7 @@ int main(int argc, char** argv) {
         {"test_expected_message_len", test_expected_message_len},
         {"test_batch_round_trip", test_batch_round_trip},
         {"test_stream_framing", test_stream_framing},
+        {"test_stream_stage_size", test_stream_stage_size},
         {"test_auth_unix_flavors", test_auth_unix_flavors},
         {"test_auth_opaque_flavors", test_auth_opaque_flavors},
         {"test_auth_unix_params", test_auth_unix_params},

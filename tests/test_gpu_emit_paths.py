@@ -19,9 +19,9 @@ pytestmark = pytest.mark.gpu
 # ws: the wave-specialised kernel, which runs header-heavy batches as
 # wave-per-tile workers (encode.hip ws_header_heavy); ws_pipeline: the same
 # kernel with that fallback off (0x10000), its producer/consumer pipeline
-# on every shape; tile: the wave-per-tile kernel; tile_preload: the same with
-# the AUTH_UNIX credential block preloaded (0x80000, lab)
-PATHS = {"ws": 0x200, "ws_pipeline": 0x10200, "tile": 0x400, "tile_preload": 0x80400}
+# on every shape; tile: the wave-per-tile kernel; tile_replan: the same
+# re-planning each record instead of reading the plan's lengths (0x20000)
+PATHS = {"ws": 0x200, "ws_pipeline": 0x10200, "tile": 0x400, "tile_replan": 0x20400}
 
 
 @pytest.fixture(scope="module")

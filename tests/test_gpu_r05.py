@@ -365,36 +365,6 @@ def test_c4_device_byte_check_across_chunks(R):
 
 
 # ---------------------------------------------------------------------------
-# single pass (ONC_VARIANT_SINGLE_PASS, lab): no enc_len launch
-# ---------------------------------------------------------------------------
-@pytest.mark.parametrize("claim", ["wave", "workgroup", "block_order", "workgroup_wgl", "block_order_wgl", "wg8"])
-@pytest.mark.parametrize("kind", ["mixed", "unix16", "adversarial", "call_none"])
-def test_single_pass_encode_bit_exact(R, oracle, kind, claim):
-    """The single-pass encode (tiles claimed in start order — per wave, per
-    workgroup, or in blockIdx order without a claim — placed by a decoupled
-    look-back per tile or per workgroup inside the wave-per-tile enc_emit) produces the oracle's bytes,
-    offsets, statuses and lengths — at two writer positions and with a
-    capacity inside the batch — and its output decodes."""
-    from test_gpu_emit_paths import _enc_oracle_sized, _adversarial
-    hb = {"mixed": lambda: S.mixed(70_001, seed=91, pmin=0, pmax=900, exotic=0.2),
-          "unix16": lambda: S.call_unix16(50_000, 64, seed=92),
-          "adversarial": lambda: _adversarial(93, n=5000),
-          "call_none": lambda: S.call_none(300_000, 256, seed=94)}[kind]()
-    extra = {"wave": 0, "workgroup": R.VARIANT_SP_WG_CLAIM, "block_order": R.VARIANT_SP_BLOCK_ORDER,
-             "workgroup_wgl": R.VARIANT_SP_WG_CLAIM | R.VARIANT_SP_WG_LOOKBACK,
-             "block_order_wgl": R.VARIANT_SP_BLOCK_ORDER | R.VARIANT_SP_WG_LOOKBACK,
-             "wg8": R.VARIANT_SP_WG8}[claim]
-    c = R.Codec(0, variant=R.VARIANT_SINGLE_PASS | extra)
-    try:
-        o_st, o_len = _enc_oracle_sized(R, c, hb, oracle)
-        _enc_oracle_sized(R, c, hb, oracle, shift=5)
-        total = int(o_len.astype(np.int64).sum())
-        _enc_oracle_sized(R, c, hb, oracle, shift=3, cap=total // 3 + 7)
-    finally:
-        c.close()
-
-
-# ---------------------------------------------------------------------------
 # small batches (<= 512 records): one enc_emit_single_kernel launch, no
 # length pass (codec.hip small_batch) — the default path, every content kind
 # ---------------------------------------------------------------------------

@@ -33,7 +33,7 @@ def test_library_exports_every_header_symbol():
     import onc_rpc_amd.runtime as R
     assert sorted(R.EXPORTED) == funcs
     lib.onc_abi_version.restype = C.c_int
-    assert lib.onc_abi_version() == R.ABI_VERSION == 7
+    assert lib.onc_abi_version() == R.ABI_VERSION == 8
     lib.onc_status_str.restype = C.c_char_p
     assert lib.onc_status_str(1) == b"incomplete rpc message"
 

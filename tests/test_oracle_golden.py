@@ -5,6 +5,8 @@ tests with citations) and to independent xdrlib-built messages.
 These mirror the reference tests they cite: decode → field asserts →
 serialise → byte equality.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -298,3 +300,70 @@ def test_declared_extent_placeholder(oracle):
     ms, _, ss, a0, _ = oracle.decode_batch(np.frombuffer(wire + b"\0" * 16, np.uint8), fo, L.DECODE_SLICE)
     assert list(ss) == [0, 11, 0, 0] and int(a0[1]) == 0      # the placeholder: InvalidRpcVersion(0)
     assert list(ms["xid"][[0, 2, 3]]) == [1, 5, 7]
+
+
+def _expected_message_len_loop(buf):
+    """The caller's framing loop over a stream (rpc_message.rs:343-367),
+    restated in Python: record starts until the buffer ends."""
+    off, p = [0], 0
+    while len(buf) - p >= 4:
+        hdr = int.from_bytes(buf[p:p + 4], "big")
+        assert hdr & 0x80000000, "Fragmented"
+        p += (hdr & 0x7FFFFFFF) + 4
+        assert p <= len(buf), "IncompleteMessage"
+        off.append(p)
+    assert p == len(buf)
+    return off
+
+
+def _placeholder_batch():
+    """The descriptors of tests/golden/placeholder.json (make_placeholder.py)."""
+    unix = {"kind": "unix", "stamp": 7, "machine_name": b"host".hex(), "uid": 1, "gid": 2, "gids": [3, 4, 5]}
+    none = {"kind": "none"}
+
+    def call(xid, cred, verf=none, payload=b"\x11" * 10):
+        return {"xid": xid, "type": "call", "program": 100003, "program_version": 4, "procedure": 1,
+                "cred": cred, "verf": verf, "payload": payload.hex()}
+    msgs = [call(1, unix), call(2, unix), call(3, unix, {"kind": "short", "data": ("ab" * 201)}),
+            call(4, unix), call(5, none),
+            {"xid": 6, "type": "reply", "reply": "accepted", "verf": unix, "accept_status": "success",
+             "payload": "22" * 5},
+            call(7, none)]
+    hb = L.build_batch(msgs, declare=True)
+    m = hb.msgs
+    ref = lambda i, f="cred": int(m[f + "_ref"][i])          # noqa: E731
+    hb.unix["ngids"][ref(1)] = 17
+    hb.unix["ngids"][ref(2)] = 17
+    m["cred_kind_len"][3] = int(L.pack_kind_len(L.KIND_UNIX, 0))
+    hb.unix["ngids"][ref(3)] = 17
+    hb.unix["name_len"][ref(5, "verf")] = 300
+    return hb
+
+
+def placeholder_fixture():
+    import json
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "placeholder.json")) as f:
+        return json.load(f)
+
+
+def test_placeholder_and_compaction_fixture(oracle):
+    """tests/golden/placeholder.json (struct.pack, no oracle) pins the
+    placeholder bytes of the batch encode (ABI 7) and the compacted stream
+    (onc_compact, ABI 8): the oracle's encode and oracle_compact reproduce
+    them byte for byte; a Python restatement of the caller's
+    expected_message_len loop (rpc_message.rs:343-367) frames the encode's
+    stream into the records with an extent and the compacted one into exactly
+    the OK messages."""
+    fx = placeholder_fixture()
+    hb = _placeholder_batch()
+    wire, off, st, _ = oracle.encode_batch(hb)
+    assert list(st) == fx["status"]
+    assert wire.hex() == fx["wire"]
+    assert list(off) == fx["rec_off"]
+    w = bytes.fromhex(fx["wire"])
+    has = np.diff(np.asarray(fx["rec_off"])) != 0
+    assert _expected_message_len_loop(w) == list(np.asarray(fx["rec_off"])[:-1][has]) + [len(w)]
+    cw, coff = oracle.compact(wire, off, st)
+    assert cw.hex() == fx["compacted"] and list(coff) == fx["compacted_rec_off"]
+    c = bytes.fromhex(fx["compacted"])
+    assert len(_expected_message_len_loop(c)) - 1 == int((np.asarray(fx["status"]) == 0).sum())
