@@ -187,7 +187,8 @@ def cpu_available():
 
 def native_oracle():
     """The oracle compiled -O3 -march=native for THIS host (BASELINE.md's
-    CPU-baseline build), cached per CPU model/flags under oracle/_native.
+    CPU-baseline build), cached per CPU model/flags and oracle source under
+    oracle/_native.
     Returns (path, flags) or (None, reason) when gcc is unavailable."""
     import hashlib
     try:
@@ -195,7 +196,11 @@ def native_oracle():
             first = f.read().split("\n\n")[0]
     except OSError:
         first = ""
-    key = hashlib.sha1(first.encode()).hexdigest()[:12]
+    h = hashlib.sha1(first.encode())
+    for src in ("onc_oracle.c", "onc_oracle.h"):      # a source change rebuilds it
+        with open(os.path.join(ROOT, "oracle", src), "rb") as f:
+            h.update(f.read())
+    key = h.hexdigest()[:12]
     d = os.path.join(ROOT, "oracle", "_native", key)
     so = os.path.join(d, "liboncoracle.so")
     flags = ["-O3", "-march=native", "-std=c11", "-fPIC", "-shared"]
