@@ -606,6 +606,9 @@ def pcie_zero_copy(args, torch, R, wl, hb, codec, out, total_bytes, lens_np, rec
             ok = check_dec()
             if args.frame:
                 ok = ok and [int(x) for x in fres.cpu()[:3]] == [n, total_bytes, 0]
+            if not args.frame:
+                res["variants"] = c2_zero_copy_variants(args, torch, R, codec, w, rl, o, n, n_total, total_bytes,
+                                                        mode, check_dec)
             rd = int(parsed_lines_bytes(lens_np))
             res.update({"value": n_total / (ms / 1e3) / 1e6, "ms_per_step": ms, "validated": ok,
                         "h2d_bytes_touched_per_gpu": rd + (0 if args.frame else 4 * n),
@@ -677,6 +680,79 @@ def pcie_zero_copy(args, torch, R, wl, hb, codec, out, total_bytes, lens_np, rec
         torch.cuda.synchronize()
         for k in keep:
             k.close()
+
+
+def c2_zero_copy_variants(args, torch, R, codec, w, rl, o, n, n_total, total_bytes, mode, check_dec):
+    """What else a server pays or picks on the c2 zero-copy decode
+    (VERDICT r05 item 3):
+    register_per_batch — the socket buffer NOT registered beforehand: every
+      step pins it (onc_host_register of the 1.9 GB wire and of its lengths),
+      decodes it in place, synchronises and unpins it; host wall clock (the
+      registration is synchronous host work). The data is written into the
+      buffer before the timed loop (the pages are resident, as after a recv).
+    policy_standard / policy_line / policy_auto — the same registered-once
+      decode under each first-round policy pinned (onc_codec_set_decode_policy):
+      STANDARD fetches each record's first 44 bytes (a 64-byte span), LINE the
+      rest of its first 128-byte line; over PCIe every fetched granule crosses
+      the link."""
+    import ctypes as C
+    import mmap
+    import time
+    import numpy as np
+    out = {}
+    reps = max(1, args.pcie_reps)
+    for name, pol in (("policy_standard", R.DECODE_POLICY_STANDARD), ("policy_line", R.DECODE_POLICY_LINE),
+                      ("policy_auto", R.DECODE_POLICY_AUTO)):
+        codec.set_decode_policy(pol)
+
+        def step():
+            codec.decode_lengths(w, rl, n, 0, mode, o.msgs, o.unix, o.status, o.aux0, o.aux1, rec_off=o.off)
+        ms = _event_ms(torch, step, reps)
+        out[name] = {"value": n_total / (ms / 1e3) / 1e6, "ms_per_step": ms, "validated": check_dec()}
+    codec.set_decode_policy(R.DECODE_POLICY_AUTO)
+    # register per batch: a plain (unpinned) buffer holding the same bytes
+    mm = mmap.mmap(-1, total_bytes + 16 + 4096)
+    mm_l = mmap.mmap(-1, 4 * n + 4096)
+    hb_w = hb_l = None
+    try:
+        hb_w = np.frombuffer(mm, np.uint8, count=total_bytes + 16)
+        hb_w[:] = w.host[:total_bytes + 16]
+        hb_l = np.frombuffer(mm_l, np.uint8, count=4 * n)
+        hb_l[:] = rl.host[:4 * n]
+        aw, al = hb_w.ctypes.data, hb_l.ctypes.data
+        lib = codec.lib
+
+        class _Dev:
+            def __init__(self, p):
+                self.p = p
+
+            def data_ptr(self):
+                return self.p
+
+        def step():
+            dw, dl = C.c_void_p(), C.c_void_p()
+            codec._check(lib.onc_host_register(codec.h, C.c_void_p(aw), total_bytes + 16, C.byref(dw)), "register")
+            codec._check(lib.onc_host_register(codec.h, C.c_void_p(al), 4 * n, C.byref(dl)), "register")
+            codec.decode_lengths(_Dev(dw.value), _Dev(dl.value), n, 0, mode, o.msgs, o.unix, o.status, o.aux0,
+                                 o.aux1, rec_off=o.off)
+            codec.sync()
+            codec._check(lib.onc_host_unregister(codec.h, C.c_void_p(aw)), "unregister")
+            codec._check(lib.onc_host_unregister(codec.h, C.c_void_p(al)), "unregister")
+        step()
+        r = max(2, min(reps, 5))
+        t0 = time.perf_counter()
+        for _ in range(r):
+            step()
+        ms = (time.perf_counter() - t0) * 1e3 / r
+        out["register_per_batch"] = {
+            "value": n_total / (ms / 1e3) / 1e6, "ms_per_step": ms, "validated": check_dec(),
+            "note": f"onc_host_register of the {total_bytes}-byte wire + its lengths, the in-place decode, a "
+                    "synchronisation and onc_host_unregister per step (host wall clock)"}
+    finally:
+        del hb_w, hb_l
+        mm.close()
+        mm_l.close()
+    return out
 
 
 def iov_gather_ok(hdr, e, payload, ref_wire, wire_base=0, step=1 << 16):
@@ -1431,7 +1507,9 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
         zc = pcie_zero_copy(args, torch, R, wl, hb, codec, out, total_bytes, lens_np, rec_off, dec_off, dec, mode,
                             n_total, bool((kinds == L.KIND_UNIX).any()))
         if wl == "c2":
-            zc = reduce_leg(torch, dist, dev, zc, [""], n_total)
+            zc = reduce_leg(torch, dist, dev, zc, [""] + ([] if args.frame else [
+                "variants.register_per_batch", "variants.policy_standard", "variants.policy_line",
+                "variants.policy_auto"]), n_total)
         else:
             zc.setdefault("variants", {})
             zc = reduce_leg(torch, dist, dev, zc, ["variants.in_place", "variants.wire_on_device"], n_total)
@@ -1511,6 +1589,34 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
     return result
 
 
+def host_pinned_peak(dist, world):
+    """Peak pinned host memory of this run: torch's pinned allocator (the
+    staging legs' pin_memory buffers) + the host ranges registered through
+    runtime.HostMapped (the zero-copy legs), per rank and summed over the
+    ranks that share this host (the sum of per-rank peaks bounds the
+    simultaneous total from above)."""
+    import torch
+    R = sys.modules.get("onc_rpc_amd.runtime")
+    if R is None or not torch.cuda.is_available():          # (--check-launch: no GPU legs ran)
+        return None
+    st = torch.cuda.host_memory_stats() if hasattr(torch.cuda, "host_memory_stats") else {}
+    tp = 0
+    for k in ("allocated_bytes.peak", "reserved_bytes.peak", "allocated_bytes.all.peak"):
+        if k in st:
+            tp = max(tp, int(st[k]))
+    mine = float(tp + R.HostMapped.peak_bytes)
+    out = {"per_rank_peak_bytes": mine, "torch_pinned_peak_bytes": tp, "host_mapped_peak_bytes": R.HostMapped.peak_bytes}
+    if dist is not None and world > 1:
+        t = torch.tensor([mine, mine], dtype=torch.float64, device=cdev(torch.cuda.current_device()))
+        s = t.clone()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        out.update({"per_rank_peak_bytes_max": float(t[0]), "sum_over_ranks_bytes": float(s[0])})
+    else:
+        out["sum_over_ranks_bytes"] = mine
+    return out
+
+
 def finish(args, result, pending, dist, rank, world):
     """Closing step of every run: with N > 1 ranks, rank 0 times the CPU
     baseline (`pending`: the arguments cpu_baseline needs) only after every
@@ -1518,6 +1624,7 @@ def finish(args, result, pending, dist, rank, world):
     then rank 0 prints the one JSON line."""
     if dist is not None:
         dist.barrier()                  # every rank's GPU legs are done
+    result["host_pinned"] = host_pinned_peak(dist, world)
     if pending is not None:
         cb = cpu_baseline(args, *pending)
         if world > 1:

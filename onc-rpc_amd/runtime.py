@@ -348,8 +348,14 @@ class HostMapped:
     address, so it goes wherever a device tensor goes in this binding
     (Codec calls, DeviceBatch fields). close() unregisters it."""
 
+    # bytes registered through HostMapped in this process, now and at most
+    # (bench.py reports the pinned host memory a run holds)
+    live_bytes = 0
+    peak_bytes = 0
+
     def __init__(self, codec: "Codec", nbytes: int):
         self.nbytes = int(nbytes)
+        self._dev = None
         self._mm = mmap.mmap(-1, max(self.nbytes, 4096))
         self.host = np.frombuffer(self._mm, np.uint8, count=self.nbytes)
         self._addr = self.host.ctypes.data if self.nbytes else np.frombuffer(self._mm, np.uint8).ctypes.data
@@ -358,6 +364,8 @@ class HostMapped:
         codec._check(codec.lib.onc_host_register(codec.h, C.c_void_p(self._addr), max(self.nbytes, 4096),
                                                   C.byref(dev)), "onc_host_register")
         self._dev = dev.value
+        HostMapped.live_bytes += max(self.nbytes, 4096)
+        HostMapped.peak_bytes = max(HostMapped.peak_bytes, HostMapped.live_bytes)
 
     @classmethod
     def from_array(cls, codec, arr):
@@ -385,6 +393,7 @@ class HostMapped:
         # the pages are unpinned before the mapping is freed
         if self._dev is not None:
             self._codec.lib.onc_host_unregister(self._codec.h or None, C.c_void_p(self._addr))
+            HostMapped.live_bytes -= max(self.nbytes, 4096)
         self._dev = None
 
     def __del__(self):

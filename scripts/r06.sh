@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-6 GPU steps (one call runs several; every GPU step has its own
+# timeout; the script stops at the first crash, abort or timeout):
+#   first     the GPU suite, then (suite passed or only failed tests) the
+#             look-back diagnosis and link labs, then (suite green) the
+#             producer/consumer decode A/B (scripts/ab.sh)
+#   ab        the decode A/B only (WLS, ROUNDS)
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step=${1:-first}; shift || true
+crash() { [ "$1" -gt 1 ] && [ "$1" -ne 3 ]; }     # pytest 1 = failed tests; bench 3 = not validated
+case $step in
+  first)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread \
+      > gpurun_out/tests.log 2>&1; rc=$?
+    grep -E "passed|failed|error" gpurun_out/tests.log | tail -3; echo "tests rc=$rc"
+    crash $rc && exit $rc
+    timeout -k 10 120 tools/lookback_diag > gpurun_out/lookback_diag.log 2>&1; r=$?; echo "diag rc=$r"; crash $r && exit $r
+    timeout -k 10 180 tools/link_lab > gpurun_out/link_lab.log 2>&1; r=$?; echo "link rc=$r"; crash $r && exit $r
+    [ $rc -eq 0 ] || exit $rc
+    CASES="prod:onc-rpc_amd/libonc_rpc_amd.so:0 pc:onc-rpc_amd/libonc_rpc_amd.so:0x80000" WLS="${WLS:-c1 c0 c2 c3}" \
+      ROUNDS=${ROUNDS:-2} TESTS=0 bash scripts/ab.sh > gpurun_out/ab_pc.log 2>&1; r=$?; cat gpurun_out/ab_pc.log; exit $r ;;
+  ab)
+    CASES="prod:onc-rpc_amd/libonc_rpc_amd.so:0 pc:onc-rpc_amd/libonc_rpc_amd.so:0x80000" WLS="${WLS:-c1 c0 c2 c3}" \
+      ROUNDS=${ROUNDS:-2} TESTS=0 bash scripts/ab.sh > gpurun_out/ab_pc.log 2>&1; r=$?; cat gpurun_out/ab_pc.log; exit $r ;;
+esac
