@@ -858,17 +858,24 @@ struct PcSlot {
 template <int kChunks, int kSlots>
 struct PcShared {
     PcSlot<kChunks> slot[kSlots];
+    // a consumer's second-round rows (granules kChunks .. kWinChunks - 1 of
+    // the records whose header reaches past the first round), same layout
+    uint32_t ovf[kPcConsumers][(kWinChunks - kChunks) * 256];
     uint32_t filled[kSlots];
     uint32_t freed[kSlots];
 };
 
-template <bool kAligned>
+template <bool kAligned, int kChunks>
 struct RdRaw {
     uintptr_t base;          // absolute address of record byte 0
     uint32_t lim;            // record bytes held by the rows
     uint32_t q0;             // record byte 0's offset in its first granule
     const uint32_t* row;     // the slot's rows + lane * 4
-    __device__ __forceinline__ uint32_t word(uint32_t d) const { return row[(d >> 2) * 256 + (d & 3)]; }
+    const uint32_t* ovf;     // the consumer's second-round rows + lane * 4
+    __device__ __forceinline__ uint32_t word(uint32_t d) const {
+        const uint32_t r = d >> 2;
+        return r < uint32_t(kChunks) ? row[r * 256 + (d & 3)] : ovf[(r - kChunks) * 256 + (d & 3)];
+    }
     __device__ __forceinline__ uint32_t be32(uint32_t pos) const {
         if (pos + 4u <= lim) {
             const uint32_t g = q0 + pos;
@@ -978,19 +985,39 @@ __device__ __forceinline__ uint32_t pc_header_need(const RdT& R, uint64_t L) {
 }
 
 template <int MODE, bool kAligned, int kChunks>
-__device__ __forceinline__ void pc_consume(const DecArgs& a, PcSlot<kChunks>& S, uint64_t tile) {
+__device__ __forceinline__ void pc_consume(const DecArgs& a, PcSlot<kChunks>& S, uint32_t* ovf, uint64_t tile) {
     const int t = threadIdx.x & 63;
     const uint64_t i0 = tile * 64;
     const uint64_t i = i0 + t;
     const bool valid = i < a.n;
     const uint64_t b = S.b[t], L = S.L[t];
     const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire) + b;
+    const uintptr_t win = base & ~uintptr_t(15);
     const uint32_t q0 = uint32_t(base & 15);
-    const uint64_t avail = min(uint64_t(kChunks), (q0 + L + 15) >> 4);
-    const RdRaw<kAligned> R{base, L ? uint32_t(16 * avail) - q0 : 0u, q0, S.win + 4 * t};
+    const uint64_t avail = min(uint64_t(kWinChunks), (q0 + L + 15) >> 4);     // granules of the record, capped
+    const uint32_t r1 = uint32_t(min(uint64_t(kChunks), avail));            // loaded by the loader
+    const RdRaw<kAligned, kChunks> R1{base, L ? 16 * r1 - q0 : 0u, q0, S.win + 4 * t, ovf + 4 * t};
+    // header extent from the first round; the granules past it (rare under
+    // the line policy; AUTH_UNIX calls under the standard one) in one round
+    // trip into this consumer's second-round rows
+    const uint32_t need = valid && L ? pc_header_need(R1, L) : 0u;
+    const uint32_t want = valid && L ? uint32_t(min(avail, uint64_t((q0 + need + 15) >> 4))) : 0u;
+    const uint32_t got = max(want, r1);
+    if (__any(want > r1)) {
+        constexpr int kN2 = int(kWinChunks) - kChunks;
+        u32x4 v[kN2 > 0 ? kN2 : 1];
+#pragma unroll
+        for (int c = 0; c < kN2; ++c)
+            if (uint32_t(kChunks + c) < want) v[c] = gload<u32x4>(win + 16 * uint32_t(kChunks + c));
+#pragma unroll
+        for (int c = 0; c < kN2; ++c)
+            if (uint32_t(kChunks + c) < want) *reinterpret_cast<u32x4*>(ovf + c * 256 + 4 * t) = v[c];
+        wave_sync_lds();
+    }
+    const RdRaw<kAligned, kChunks> R{base, L ? 16 * got - q0 : 0u, q0, S.win + 4 * t, ovf + 4 * t};
     if ((tile & 63) == 0 && a.hint) {
-        const bool needs2 = valid && L != 0 && (q0 + pc_header_need(R, L) + 15) / 16 >
-                                                     min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4);
+        const bool needs2 = valid && L != 0 && (q0 + need + 15) / 16 >
+                                                   min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4);
         const uint32_t cnt = uint32_t(__popcll(__ballot(needs2)));
         if (t == 0) __hip_atomic_store(a.hint, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -1146,8 +1173,9 @@ __global__ __launch_bounds__(64 * (1 + kPcConsumers)) void decode_pc_kernel(DecA
         PcSlot<kChunks>& S = sh.slot[s];
         const uint64_t tile = blockIdx.x + j * G;
         const bool aligned = __all(((reinterpret_cast<uintptr_t>(a.wire) + S.b[t]) & 3) == 0);
-        if (aligned) pc_consume<MODE, true>(a, S, tile);
-        else pc_consume<MODE, false>(a, S, tile);
+        uint32_t* ovf = sh.ovf[wv - 1];
+        if (aligned) pc_consume<MODE, true>(a, S, ovf, tile);
+        else pc_consume<MODE, false>(a, S, ovf, tile);
         lds_publish(&sh.freed[s], use + 1u);
     }
 }

@@ -21,6 +21,16 @@ case $step in
     [ $rc -eq 0 ] || exit $rc
     CASES="prod:onc-rpc_amd/libonc_rpc_amd.so:0 pc:onc-rpc_amd/libonc_rpc_amd.so:0x80000" WLS="${WLS:-c1 c0 c2 c3}" \
       ROUNDS=${ROUNDS:-2} TESTS=0 bash scripts/ab.sh > gpurun_out/ab_pc.log 2>&1; r=$?; cat gpurun_out/ab_pc.log; exit $r ;;
+  sqlds)
+    # LDS counters of the configs[0] encode: one --pmc pass, kernel trace only
+    wl=${1:-c0}
+    OUT=$PWD/gpurun_out
+    P="SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_INSTS_VALU"
+    timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $P -d $OUT/sqlds_$wl -o run --output-format csv -- \
+      python3 bench.py --workload $wl --steps 3 --warmup 1 --no-cpu-baseline --no-pcie --c4-leg off --iov-leg off \
+      --cache-leg off > $OUT/sqlds_$wl.log 2>&1; r=$?; echo "sqlds rc=$r"; [ $r -eq 0 ] || exit $r
+    python3 scripts/sq_json.py $OUT/sqlds_$wl.json "rocprofv3 --kernel-trace --pmc (LDS pass) over bench.py --workload $wl --steps 3 --warmup 1" \
+      $(ls $OUT/sqlds_$wl/*counter_collection.csv) | grep onc ;;
   ab)
     CASES="prod:onc-rpc_amd/libonc_rpc_amd.so:0 pc:onc-rpc_amd/libonc_rpc_amd.so:0x80000" WLS="${WLS:-c1 c0 c2 c3}" \
       ROUNDS=${ROUNDS:-2} TESTS=0 bash scripts/ab.sh > gpurun_out/ab_pc.log 2>&1; r=$?; cat gpurun_out/ab_pc.log; exit $r ;;
