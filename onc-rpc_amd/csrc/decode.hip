@@ -890,6 +890,20 @@ struct RdRaw {
     }
 };
 
+// Round-1 granules of a record (L != 0) as decode_kernel's stage_window
+// takes them: the standard policy the chunks of the first 44 bytes; the line
+// policy also the rest of the record's first 128-byte line and at least its
+// first 128 bytes; never past the record's last granule.
+template <bool kLine>
+__device__ __forceinline__ uint32_t pc_round1(uintptr_t win, uint32_t q0, uint64_t L) {
+    const uint32_t avail = uint32_t(min(uint64_t(kWinChunks), (q0 + L + 15) >> 4));
+    const uint32_t r44 = uint32_t(min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4));
+    if (!kLine) return min(r44, avail);
+    const uint32_t rln = uint32_t((((win | 127u) + 1u) - win) >> 4);
+    const uint32_t r128 = uint32_t((q0 + min(L, uint64_t(128)) + 15) >> 4);
+    return min(min(kWin1L, max(max(r44, rln), r128)), avail);
+}
+
 __device__ __forceinline__ uint32_t lds_counter(const uint32_t* f) {
     return uint32_t(__builtin_amdgcn_readfirstlane(int(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))));
 }
@@ -995,7 +1009,7 @@ __device__ __forceinline__ void pc_consume(const DecArgs& a, PcSlot<kChunks>& S,
     const uintptr_t win = base & ~uintptr_t(15);
     const uint32_t q0 = uint32_t(base & 15);
     const uint64_t avail = min(uint64_t(kWinChunks), (q0 + L + 15) >> 4);     // granules of the record, capped
-    const uint32_t r1 = uint32_t(min(uint64_t(kChunks), avail));            // loaded by the loader
+    const uint32_t r1 = L ? pc_round1<(kChunks > int(kWin1))>(win, q0, L) : 0u;   // loaded by the loader
     const RdRaw<kAligned, kChunks> R1{base, L ? 16 * r1 - q0 : 0u, q0, S.win + 4 * t, ovf + 4 * t};
     // header extent from the first round; the granules past it (rare under
     // the line policy; AUTH_UNIX calls under the standard one) in one round
@@ -1004,14 +1018,20 @@ __device__ __forceinline__ void pc_consume(const DecArgs& a, PcSlot<kChunks>& S,
     const uint32_t want = valid && L ? uint32_t(min(avail, uint64_t((q0 + need + 15) >> 4))) : 0u;
     const uint32_t got = max(want, r1);
     if (__any(want > r1)) {
-        constexpr int kN2 = int(kWinChunks) - kChunks;
-        u32x4 v[kN2 > 0 ? kN2 : 1];
+        // granules [r1, want): rows below kChunks are this lane's own slots
+        // in the slot's rows (the consumer owns the slot), the rest go to its
+        // second-round rows
+        u32x4 v[kWinChunks];
 #pragma unroll
-        for (int c = 0; c < kN2; ++c)
-            if (uint32_t(kChunks + c) < want) v[c] = gload<u32x4>(win + 16 * uint32_t(kChunks + c));
+        for (uint32_t c = 0; c < kWinChunks; ++c)
+            if (c >= r1 && c < want) v[c] = gload<u32x4>(win + 16 * c);
 #pragma unroll
-        for (int c = 0; c < kN2; ++c)
-            if (uint32_t(kChunks + c) < want) *reinterpret_cast<u32x4*>(ovf + c * 256 + 4 * t) = v[c];
+        for (uint32_t c = 0; c < kWinChunks; ++c) {
+            if (c >= r1 && c < want) {
+                uint32_t* dst = c < uint32_t(kChunks) ? S.win + c * 256 + 4 * t : ovf + (c - kChunks) * 256 + 4 * t;
+                *reinterpret_cast<u32x4*>(dst) = v[c];
+            }
+        }
         wave_sync_lds();
     }
     const RdRaw<kAligned, kChunks> R{base, L ? 16 * got - q0 : 0u, q0, S.win + 4 * t, ovf + 4 * t};
@@ -1139,16 +1159,14 @@ __global__ __launch_bounds__(64 * (1 + kPcConsumers)) void decode_pc_kernel(DecA
                 S.L[t] = LL[k];
                 const uintptr_t ab = wire + bb[k];
                 const uintptr_t win = ab & ~uintptr_t(15);
-                const uint64_t q0 = ab & 15;
-                const uintptr_t last = win + 16 * ((q0 + LL[k] + 15) / 16 - 1);
-                if (LL[k] != 0) {
+                const uint32_t q0 = uint32_t(ab & 15);
+                const uint32_t r1 = LL[k] != 0 ? pc_round1<kLine>(win, q0, LL[k]) : 0u;
 #pragma unroll
-                    for (int c = 0; c < kChunks; ++c) {
-                        const uintptr_t src = min(win + 16 * uint64_t(c), last);
-                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const ONC_GLOBAL void*>(src),
+                for (int c = 0; c < kChunks; ++c) {
+                    if (uint32_t(c) < r1)
+                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const ONC_GLOBAL void*>(win + 16 * uint32_t(c)),
                                                          (__attribute__((address_space(3))) void*)(S.win + 256 * c),
                                                          16, 0, 0);
-                    }
                 }
             }
 #pragma unroll

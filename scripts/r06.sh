@@ -31,6 +31,16 @@ case $step in
       --cache-leg off > $OUT/sqlds_$wl.log 2>&1; r=$?; echo "sqlds rc=$r"; [ $r -eq 0 ] || exit $r
     python3 scripts/sq_json.py $OUT/sqlds_$wl.json "rocprofv3 --kernel-trace --pmc (LDS pass) over bench.py --workload $wl --steps 3 --warmup 1" \
       $(ls $OUT/sqlds_$wl/*counter_collection.csv) | grep onc ;;
+  8rank)
+    # the driver's 8-GPU command rehearsed with 8 ranks on this one GPU (gloo control plane);
+    # a heartbeat file shows progress while the ranks run
+    (while sleep 45; do date +%T >> gpurun_out/heartbeat_8rank.log; done) & hb=$!
+    s0=$(date +%s)
+    ONC_BENCH_SAME_DEVICE=1 timeout -k 10 1000 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+      --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 8 --backend gloo \
+      > gpurun_out/bench_8ranks_same_device.log 2>&1; r=$?
+    kill $hb 2>/dev/null
+    echo "8 ranks rc=$r wall_s=$(( $(date +%s) - s0 ))" | tee -a gpurun_out/bench_8ranks_same_device.log; exit $r ;;
   ab)
     CASES="prod:onc-rpc_amd/libonc_rpc_amd.so:0 pc:onc-rpc_amd/libonc_rpc_amd.so:0x80000" WLS="${WLS:-c1 c0 c2 c3}" \
       ROUNDS=${ROUNDS:-2} TESTS=0 bash scripts/ab.sh > gpurun_out/ab_pc.log 2>&1; r=$?; cat gpurun_out/ab_pc.log; exit $r ;;
