@@ -579,9 +579,10 @@ int onc_encode_iov(onc_codec* codec, const onc_batch* batch,
  * other failing record already takes 0 bytes, so a batch without a
  * placeholder moves nothing. `status` is onc_encode's. Bytes from the new
  * rec_off[n] up to the old one are left as they were. *total (host,
- * optional) receives the new rec_off[n]. Synchronous (it sizes its scratch
- * by the moved bytes, which it reads back): ONC_RC_ECAPTURE inside a stream
- * capture. Launches only when the caller saw a failing status. */
+ * optional) receives the new rec_off[n]. Synchronous: it sizes its scratch
+ * by the moved bytes, which it reads back, and returns with the buffer and
+ * rec_off final (ONC_RC_ECAPTURE inside a stream capture). For the rare
+ * path: call it only after seeing a failing status. */
 int onc_compact(onc_codec* codec, uint8_t* out, uint64_t* rec_off, const int32_t* status, uint64_t n,
                 uint64_t* total);
 

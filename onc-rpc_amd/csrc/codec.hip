@@ -1088,8 +1088,11 @@ int onc_compact(onc_codec* c, uint8_t* out, uint64_t* rec_off, const int32_t* st
         e = hipMemcpyAsync(out + lo, c->cmp_bytes, moved, hipMemcpyDefault, c->stream);   // (out may be mapped host memory)
         if (e != hipSuccess) return fail(c, e, "hipMemcpyAsync");
     }
-    return run(c, ONC_K_COMPACT, "compact_offsets",
-               [&] { return onc::launch_compact_offsets(rec_off, c->cmp_off, fb, n, base, c->stream); });
+    rc = run(c, ONC_K_COMPACT, "compact_offsets",
+             [&] { return onc::launch_compact_offsets(rec_off, c->cmp_off, fb, n, base, c->stream); });
+    if (rc != ONC_RC_OK) return rc;
+    e = hipStreamSynchronize(c->stream);             // synchronous: the buffer is final on return
+    return e == hipSuccess ? ONC_RC_OK : fail(c, e, "hipStreamSynchronize");
 }
 
 int onc_compact_iov(onc_codec* c, onc_iov_rec* iov, const int32_t* status, uint64_t n, uint64_t* totals) {

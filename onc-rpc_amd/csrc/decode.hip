@@ -907,8 +907,12 @@ __device__ __forceinline__ uint32_t pc_round1(uintptr_t win, uint32_t q0, uint64
 __device__ __forceinline__ uint32_t lds_counter(const uint32_t* f) {
     return uint32_t(__builtin_amdgcn_readfirstlane(int(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))));
 }
+// Every lane stores the same value (no lane-0-only region): a store under
+// `if (lane == 0)` at the end of a loop body, followed by a readfirstlane at
+// the top of the next iteration, is the shape round 5's look-back lab was
+// miscompiled into an endless loop from (tools/lookback_diag.hip).
 __device__ __forceinline__ void lds_publish(uint32_t* f, uint32_t v) {
-    if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

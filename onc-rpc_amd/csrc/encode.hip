@@ -601,24 +601,23 @@ __device__ __forceinline__ uint32_t lds_flag(const uint32_t* f) {
 }
 template <int kGW>
 __device__ __forceinline__ uint64_t wg_place(WgPlace<kGW>& X, uint64_t tile, uint64_t agg, uint64_t ntiles) {
-    const int lane = threadIdx.x & 63;
     const int w = int(tile % kGW);
     const int live = int(min(uint64_t(kGW), ntiles - tile / kGW * kGW));
+    // (every lane stores the same wave-uniform values: no lane-0-only
+    // regions next to the readfirstlane waits, tools/lookback_diag.hip)
     if (w != 0) {
-        if (lane == 0) {
-            X.agg[w] = agg;
-            __hip_atomic_store(&X.ready[w], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        X.agg[w] = agg;
+        __hip_atomic_store(&X.ready[w], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         while (__builtin_amdgcn_readfirstlane(int(lds_flag(&X.ready[0]))) == 0) __builtin_amdgcn_s_sleep(1);
         return X.base[w];
     }
     uint64_t run = agg;
     for (int v = 1; v < live; ++v) {
         while (__builtin_amdgcn_readfirstlane(int(lds_flag(&X.ready[v]))) == 0) __builtin_amdgcn_s_sleep(1);
-        if (lane == 0) X.base[v] = run;
+        X.base[v] = run;
         run += X.agg[v];
     }
-    if (lane == 0) __hip_atomic_store(&X.ready[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&X.ready[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     return 0;
 }
 
