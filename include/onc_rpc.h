@@ -377,7 +377,6 @@ typedef struct onc_codec onc_codec;
 #define ONC_VARIANT_WS_PIPELINE      0x10000u  /* wave-specialised: the pipeline on header-heavy batches too */
 #define ONC_VARIANT_EMIT_REPLAN      0x20000u  /* wave-per-tile enc_emit re-plans instead of reading the plan's lengths */
 #define ONC_VARIANT_WHOLE_PLAN       0x40000u  /* plan a large batch whole instead of in chunks */
-#define ONC_VARIANT_DEC_PC           0x80000u  /* decode: the producer/consumer kernel (lab A/B, decode.hip decode_pc) */
 
 #define ONC_OPT_FORCE_SCAN 0x1u   /* always launch the separate block-scan kernels (tests of that path) */
 

@@ -39,11 +39,7 @@ constexpr uint32_t kWinWords = 4 * kWinChunks;
 #define ONC_DEC_TILE 64     // c1 decode 54.7 -> 50.2 us, c2 81 -> 78.6, c3 447 -> 468 vs 256 (profiles/lab_r02_dec_tile.log)
 #endif
 constexpr int kDecTile = ONC_DEC_TILE;
-constexpr uint32_t kSlotPass = 96;
-#ifndef ONC_PC_GRID
-#define ONC_PC_GRID 512
-#endif
-constexpr uint64_t kPcGrid = ONC_PC_GRID;   // decode_pc workgroups (2 per CU)       // AUTH_UNIX slots staged per pass (9 KiB of the window)
+constexpr uint32_t kSlotPass = 96;       // AUTH_UNIX slots staged per pass (9 KiB of the window)
 
 // The window column holds the record's words aligned to the record: column
 // word k = record bytes [4k, 4k + 4), whatever the record's byte offset in
@@ -822,406 +818,6 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// decode_pc: the message decode as a producer/consumer pipeline (lab,
-// ONC_VARIANT_DEC_PC). A persistent workgroup of 4 waves
-// walks its tiles (64 records each; tile = blockIdx.x + j * gridDim.x):
-// wave 0 (the loader) computes each tile's record offsets and pulls the
-// first round of every record's header granules straight into an LDS ring
-// slot with LDS-DMA (global_load_lds_dwordx4: granule k of the tile's 64
-// records is one 1 KiB row, [k][lane][16 B]); it keeps one group of
-// kGroup tiles in flight per wait and issues the next group's offset loads
-// behind that group's DMAs, so one memory round trip lands a whole group.
-// Waves 1-3 (the consumers) take the published tiles in turn (consumer c:
-// tiles c, c + 3, ...), parse them from LDS (RdRaw: a field at any record
-// byte is one ds_read, two + v_alignbyte for a record not 4-byte aligned)
-// and write the outputs exactly as decode_kernel does, staging them in
-// their slot's rows, then release the slot. Hand-off through per-slot LDS
-// counters (filled / freed uses): every wave of the workgroup is resident,
-// so a wait on a counter another wave of it advances always ends. Bytes of
-// a record past the round-1 rows are read from global memory by RdRaw
-// (the rare long header: a second round is not pipelined).
-// ---------------------------------------------------------------------------
-constexpr int kPcConsumers = 3;
-template <bool kLine>
-struct PcCfg {
-    static constexpr int kChunks = kLine ? 8 : 4;          // round-1 granules per record
-    static constexpr int kGroup = kLine ? 2 : 4;           // tiles per loader group
-    static constexpr int kSlots = 2 * kGroup + kPcConsumers;
-};
-template <int kChunks>
-struct PcSlot {
-    uint32_t win[kChunks * 256];
-    uint64_t b[64];
-    uint64_t L[64];
-};
-template <int kChunks, int kSlots>
-struct PcShared {
-    PcSlot<kChunks> slot[kSlots];
-    // a consumer's second-round rows (granules kChunks .. kWinChunks - 1 of
-    // the records whose header reaches past the first round), same layout
-    uint32_t ovf[kPcConsumers][(kWinChunks - kChunks) * 256];
-    uint32_t filled[kSlots];
-    uint32_t freed[kSlots];
-};
-
-template <bool kAligned, int kChunks>
-struct RdRaw {
-    uintptr_t base;          // absolute address of record byte 0
-    uint32_t lim;            // record bytes held by the rows
-    uint32_t q0;             // record byte 0's offset in its first granule
-    const uint32_t* row;     // the slot's rows + lane * 4
-    const uint32_t* ovf;     // the consumer's second-round rows + lane * 4
-    __device__ __forceinline__ uint32_t word(uint32_t d) const {
-        const uint32_t r = d >> 2;
-        return r < uint32_t(kChunks) ? row[r * 256 + (d & 3)] : ovf[(r - kChunks) * 256 + (d & 3)];
-    }
-    __device__ __forceinline__ uint32_t be32(uint32_t pos) const {
-        if (pos + 4u <= lim) {
-            const uint32_t g = q0 + pos;
-            if (kAligned) return bswap(word(g >> 2));
-            return bswap(funnel(word(g >> 2), word((g >> 2) + 1), g & 3u));
-        }
-        return bswap(load4(base + pos));
-    }
-    __device__ __forceinline__ void words16(uint32_t pos, uint32_t n, uint32_t out[ONC_MAX_GIDS]) const {
-#pragma unroll
-        for (uint32_t g = 0; g < ONC_MAX_GIDS; ++g) out[g] = g < n ? be32(pos + 4u * g) : 0u;
-    }
-};
-
-// Round-1 granules of a record (L != 0) as decode_kernel's stage_window
-// takes them: the standard policy the chunks of the first 44 bytes; the line
-// policy also the rest of the record's first 128-byte line and at least its
-// first 128 bytes; never past the record's last granule.
-template <bool kLine>
-__device__ __forceinline__ uint32_t pc_round1(uintptr_t win, uint32_t q0, uint64_t L) {
-    const uint32_t avail = uint32_t(min(uint64_t(kWinChunks), (q0 + L + 15) >> 4));
-    const uint32_t r44 = uint32_t(min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4));
-    if (!kLine) return min(r44, avail);
-    const uint32_t rln = uint32_t((((win | 127u) + 1u) - win) >> 4);
-    const uint32_t r128 = uint32_t((q0 + min(L, uint64_t(128)) + 15) >> 4);
-    return min(min(kWin1L, max(max(r44, rln), r128)), avail);
-}
-
-__device__ __forceinline__ uint32_t lds_counter(const uint32_t* f) {
-    return uint32_t(__builtin_amdgcn_readfirstlane(int(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))));
-}
-// Every lane stores the same value (no lane-0-only region): a store under
-// `if (lane == 0)` at the end of a loop body, followed by a readfirstlane at
-// the top of the next iteration, is the shape round 5's look-back lab was
-// miscompiled into an endless loop from (tools/lookback_diag.hip).
-__device__ __forceinline__ void lds_publish(uint32_t* f, uint32_t v) {
-    __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0)
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Offsets of one tile's records: the loads (issued together, consumed later).
-struct PcOff {
-    uint64_t x, y;                // !kFromLen: rec_off[i], rec_off[i + 1]; kFromLen: len, workgroup total
-    uint64_t pv[kDecLenFusedBlocks / 64];
-};
-template <bool kFromLen, bool kBlkFused>
-__device__ __forceinline__ void pc_off_issue(const DecArgs& a, uint64_t tile, PcOff& o) {
-    const int t = threadIdx.x & 63;
-    const uint64_t i = tile * 64 + t;
-    const auto clamp = [](uint64_t x, uint64_t hi) { return x < hi ? x : hi; };
-    if constexpr (kFromLen) {
-        const uint64_t blk = tile / (kDecLenBlk / 64), w0 = blk * (kDecLenBlk / 64);
-        const uint64_t nwg = (a.n + 63) / 64;
-        o.x = a.rec_len[clamp(i, a.n - 1)];
-        o.y = a.tile_sum[clamp(w0 + t, nwg - 1)];
-        constexpr int kPre = kBlkFused ? int(kDecLenFusedBlocks / 64) : 1;
-#pragma unroll
-        for (int k = 0; k < kPre; ++k)
-            o.pv[k] = kBlkFused ? a.blk_sum[clamp(uint64_t(t) + 64ull * k, a.nblk - 1)] : a.blk_base[blk];
-    } else {
-        o.x = a.rec_off[clamp(i, a.n - 1)];
-        o.y = a.rec_off[clamp(i, a.n - 1) + 1];
-    }
-}
-template <bool kFromLen, bool kBlkFused>
-__device__ __forceinline__ void pc_off_finish(const DecArgs& a, uint64_t tile, const PcOff& o, uint64_t& b,
-                                              uint64_t& L) {
-    const int t = threadIdx.x & 63;
-    const uint64_t i = tile * 64 + t;
-    const bool valid = i < a.n;
-    if constexpr (kFromLen) {
-        const uint64_t blk = tile / (kDecLenBlk / 64), w0 = blk * (kDecLenBlk / 64);
-        const uint64_t len = valid ? o.x : 0;
-        const uint64_t ts = w0 + t < tile ? o.y : 0;
-        uint64_t pre = 0;
-        if constexpr (kBlkFused) {
-#pragma unroll
-            for (int k = 0; k < int(kDecLenFusedBlocks / 64); ++k) pre += uint64_t(t) + 64ull * k < blk ? o.pv[k] : 0;
-        } else {
-            pre = t == 0 ? o.pv[0] : 0;
-        }
-        const uint64_t incl = wave_incl_scan_u64(len);
-        const uint64_t wbase = a.base + lane_u64(wave_incl_scan_u64(pre + ts), 63);
-        b = wbase + incl - len;
-        L = len;
-        if (a.rec_off_out && valid) {
-            a.rec_off_out[i] = b;
-            if (i + 1 == a.n) a.rec_off_out[a.n] = b + L;
-        }
-    } else {
-        b = valid ? o.x : 0;
-        L = valid ? o.y - o.x : 0;
-    }
-}
-
-// Header extent (bytes from the record start the parse reads) from the
-// first words, as stage_window's round-2 decision: whether the standard
-// first round (44 bytes) holds it (the AUTO policy's sample).
-template <class RdT>
-__device__ __forceinline__ uint32_t pc_header_need(const RdT& R, uint64_t L) {
-    uint32_t need = uint32_t(min(L, uint64_t(16 * kWinChunks)));
-    if (L >= 36 && R.lim >= 36) {
-        const uint32_t mt = R.be32(8);
-        if (mt == ONC_MSG_CALL) {
-            const uint32_t cl = R.be32(32);
-            const uint32_t vpos = 36 + cl + pad4(cl) + 4;
-            if (cl > ONC_MAX_AUTH_LEN) need = 36;
-            else if (vpos + 4 <= R.lim && vpos + 4 <= L) {
-                const uint32_t vl = R.be32(vpos);
-                need = vpos + 4 + (vl <= ONC_MAX_AUTH_LEN ? vl + pad4(vl) : 0);
-            } else {
-                need = vpos + 4 + 16;
-            }
-        } else if (mt == ONC_MSG_REPLY) {
-            const uint32_t vl = R.be32(20);
-            need = vl <= ONC_MAX_AUTH_LEN ? 24 + vl + pad4(vl) + 12 : 24;
-        }
-    }
-    return need;
-}
-
-template <int MODE, bool kAligned, int kChunks>
-__device__ __forceinline__ void pc_consume(const DecArgs& a, PcSlot<kChunks>& S, uint32_t* ovf, uint64_t tile) {
-    const int t = threadIdx.x & 63;
-    const uint64_t i0 = tile * 64;
-    const uint64_t i = i0 + t;
-    const bool valid = i < a.n;
-    const uint64_t b = S.b[t], L = S.L[t];
-    const uintptr_t base = reinterpret_cast<uintptr_t>(a.wire) + b;
-    const uintptr_t win = base & ~uintptr_t(15);
-    const uint32_t q0 = uint32_t(base & 15);
-    const uint64_t avail = min(uint64_t(kWinChunks), (q0 + L + 15) >> 4);     // granules of the record, capped
-    const uint32_t r1 = L ? pc_round1<(kChunks > int(kWin1))>(win, q0, L) : 0u;   // loaded by the loader
-    const RdRaw<kAligned, kChunks> R1{base, L ? 16 * r1 - q0 : 0u, q0, S.win + 4 * t, ovf + 4 * t};
-    // header extent from the first round; the granules past it (rare under
-    // the line policy; AUTH_UNIX calls under the standard one) in one round
-    // trip into this consumer's second-round rows
-    const uint32_t need = valid && L ? pc_header_need(R1, L) : 0u;
-    const uint32_t want = valid && L ? uint32_t(min(avail, uint64_t((q0 + need + 15) >> 4))) : 0u;
-    const uint32_t got = max(want, r1);
-    if (__any(want > r1)) {
-        // granules [r1, want): rows below kChunks are this lane's own slots
-        // in the slot's rows (the consumer owns the slot), the rest go to its
-        // second-round rows
-        u32x4 v[kWinChunks];
-#pragma unroll
-        for (uint32_t c = 0; c < kWinChunks; ++c)
-            if (c >= r1 && c < want) v[c] = gload<u32x4>(win + 16 * c);
-#pragma unroll
-        for (uint32_t c = 0; c < kWinChunks; ++c) {
-            if (c >= r1 && c < want) {
-                uint32_t* dst = c < uint32_t(kChunks) ? S.win + c * 256 + 4 * t : ovf + (c - kChunks) * 256 + 4 * t;
-                *reinterpret_cast<u32x4*>(dst) = v[c];
-            }
-        }
-        wave_sync_lds();
-    }
-    const RdRaw<kAligned, kChunks> R{base, L ? 16 * got - q0 : 0u, q0, S.win + 4 * t, ovf + 4 * t};
-    if ((tile & 63) == 0 && a.hint) {
-        const bool needs2 = valid && L != 0 && (q0 + need + 15) / 16 >
-                                                   min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4);
-        const uint32_t cnt = uint32_t(__popcll(__ballot(needs2)));
-        if (t == 0) __hip_atomic_store(a.hint, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    onc_msg m;
-    uint4* mz = reinterpret_cast<uint4*>(&m);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);
-    uint32_t aux0 = 0, aux1 = 0;
-    int32_t st = ONC_OK;
-    UnixSlots us;
-    us.mask = 0;
-    if (valid) {
-        st = parse_record<MODE>(R, L, b, i, m, aux0, aux1, us);
-        if (st != ONC_OK) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) mz[k] = make_uint4(0, 0, 0, 0);
-        }
-        __builtin_nontemporal_store(st, a.out.status + i);
-        __builtin_nontemporal_store(aux0, a.out.aux0 + i);
-        __builtin_nontemporal_store(aux1, a.out.aux1 + i);
-    }
-    // AUTH_UNIX slots packed per tile, staged in the slot's rows (as decode_kernel)
-    constexpr uint32_t kPass = uint32_t(kChunks * 1024 / sizeof(onc_unix_params));
-    const bool okr = valid && st == ONC_OK;
-    const uint64_t bc = __ballot(okr && (us.mask & 1u)), bv = __ballot(okr && (us.mask & 2u));
-    const uint32_t nslots = uint32_t(__popcll(bc) + __popcll(bv));
-    wave_sync_lds();                                  // every lane is done with the rows
-    uint4* stg = reinterpret_cast<uint4*>(S.win);
-    if (nslots) {
-        const uint64_t below = (1ull << t) - 1;
-        const uint32_t rank = uint32_t(__popcll(bc & below) + __popcll(bv & below));
-        const uint64_t sbase = 2 * i0;
-        if (okr && (us.mask & 1u)) m.cred.ref = sbase + rank;
-        if (okr && (us.mask & 2u)) m.verf.ref = sbase + rank + (us.mask & 1u);
-        u32x4* dst = reinterpret_cast<u32x4*>(a.out.unix_params + sbase);
-        for (uint32_t p0 = 0; p0 < nslots; p0 += kPass) {
-            if (p0) wave_sync_lds();
-            if (okr) {
-#pragma unroll
-                for (uint32_t k = 0; k < 2; ++k) {
-                    const uint32_t r = rank + (k ? (us.mask & 1u) : 0u) - p0;
-                    if (((us.mask >> k) & 1u) && r < kPass) {
-                        uint4* d = stg + 6 * r;
-#pragma unroll
-                        for (int q = 0; q < 6; ++q)
-                            d[q] = make_uint4(us.w[k][4 * q], us.w[k][4 * q + 1], us.w[k][4 * q + 2], us.w[k][4 * q + 3]);
-                    }
-                }
-            }
-            wave_sync_lds();
-            const uint32_t nq = 6 * min(kPass, nslots - p0);
-            for (uint32_t q = t; q < nq; q += 64) {
-                const uint4 v = stg[q];
-                __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, dst + 6 * p0 + q);
-            }
-        }
-        wave_sync_lds();
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) stg[4 * t + k] = mz[k];
-    wave_sync_lds();
-    const uint64_t nrec = min(uint64_t(64), a.n - i0);
-    uint4* dst = reinterpret_cast<uint4*>(a.out.msgs + i0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t j = uint32_t(k * 64 + t);
-        if (j < 4 * nrec) {
-            const uint4 v = stg[j];
-            __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst + j));
-        }
-    }
-    wave_sync_lds();                                  // the rows are read: the slot can be refilled
-}
-
-template <int MODE, bool kFromLen, bool kBlkFused, bool kLine>
-__global__ __launch_bounds__(64 * (1 + kPcConsumers)) void decode_pc_kernel(DecArgs a) {
-    using Cfg = PcCfg<kLine>;
-    constexpr int kChunks = Cfg::kChunks, kGroup = Cfg::kGroup, kSlots = Cfg::kSlots;
-    __shared__ PcShared<kChunks, kSlots> sh;
-    const int wv = threadIdx.x >> 6, t = threadIdx.x & 63;
-    const uint64_t G = gridDim.x, ntiles = (a.n + 63) / 64;
-    const uint64_t J = uint64_t(blockIdx.x) < ntiles ? (ntiles - 1 - blockIdx.x) / G + 1 : 0;   // this workgroup's tiles
-    if (threadIdx.x < kSlots) {
-        sh.filled[threadIdx.x] = 0u;
-        sh.freed[threadIdx.x] = 0u;
-    }
-    __syncthreads();
-    const uintptr_t wire = reinterpret_cast<uintptr_t>(a.wire);
-    if (wv == 0) {
-        // the loader: offsets of group g + 1 issued behind group g's DMAs;
-        // one wait per group lands both
-        PcOff off[kGroup];
-#pragma unroll
-        for (int k = 0; k < kGroup; ++k)
-            if (uint64_t(k) < J) pc_off_issue<kFromLen, kBlkFused>(a, blockIdx.x + uint64_t(k) * G, off[k]);
-        for (uint64_t j0 = 0; j0 < J; j0 += kGroup) {
-            uint64_t bb[kGroup], LL[kGroup];
-#pragma unroll
-            for (int k = 0; k < kGroup; ++k)
-                if (j0 + k < J) pc_off_finish<kFromLen, kBlkFused>(a, blockIdx.x + (j0 + k) * G, off[k], bb[k], LL[k]);
-            // (the wait for those loads also landed the previous group's DMAs)
-            __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
-            if (j0) {
-#pragma unroll
-                for (int k = 0; k < kGroup; ++k) {
-                    const uint64_t j = j0 - kGroup + k;
-                    lds_publish(&sh.filled[j % kSlots], uint32_t(j / kSlots) + 1u);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < kGroup; ++k) {
-                const uint64_t j = j0 + k;
-                if (j >= J) break;
-                const int s = int(j % kSlots);
-                const uint32_t use = uint32_t(j / kSlots);
-                while (lds_counter(&sh.freed[s]) < use) __builtin_amdgcn_s_sleep(1);
-                PcSlot<kChunks>& S = sh.slot[s];
-                S.b[t] = bb[k];
-                S.L[t] = LL[k];
-                const uintptr_t ab = wire + bb[k];
-                const uintptr_t win = ab & ~uintptr_t(15);
-                const uint32_t q0 = uint32_t(ab & 15);
-                const uint32_t r1 = LL[k] != 0 ? pc_round1<kLine>(win, q0, LL[k]) : 0u;
-#pragma unroll
-                for (int c = 0; c < kChunks; ++c) {
-                    if (uint32_t(c) < r1)
-                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const ONC_GLOBAL void*>(win + 16 * uint32_t(c)),
-                                                         (__attribute__((address_space(3))) void*)(S.win + 256 * c),
-                                                         16, 0, 0);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < kGroup; ++k)
-                if (j0 + kGroup + k < J) pc_off_issue<kFromLen, kBlkFused>(a, blockIdx.x + (j0 + kGroup + k) * G, off[k]);
-        }
-        __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0): the last group landed
-        if (J) {
-            const uint64_t jl = (J - 1) / kGroup * kGroup;
-#pragma unroll
-            for (int k = 0; k < kGroup; ++k) {
-                const uint64_t j = jl + k;
-                if (j < J) lds_publish(&sh.filled[j % kSlots], uint32_t(j / kSlots) + 1u);
-            }
-        }
-        return;
-    }
-    for (uint64_t j = uint64_t(wv - 1); j < J; j += kPcConsumers) {
-        const int s = int(j % kSlots);
-        const uint32_t use = uint32_t(j / kSlots);
-        while (lds_counter(&sh.filled[s]) < use + 1u) __builtin_amdgcn_s_sleep(1);
-        PcSlot<kChunks>& S = sh.slot[s];
-        const uint64_t tile = blockIdx.x + j * G;
-        const bool aligned = __all(((reinterpret_cast<uintptr_t>(a.wire) + S.b[t]) & 3) == 0);
-        uint32_t* ovf = sh.ovf[wv - 1];
-        if (aligned) pc_consume<MODE, true>(a, S, ovf, tile);
-        else pc_consume<MODE, false>(a, S, ovf, tile);
-        lds_publish(&sh.freed[s], use + 1u);
-    }
-}
-
-template <int MODE, bool kFromLen, bool kBlkFused, bool kLine>
-hipError_t launch_pc(const DecArgs& a, hipStream_t s) {
-    const uint64_t ntiles = (a.n + 63) / 64;
-    const uint32_t g = uint32_t(min(ntiles, uint64_t(kPcGrid)));
-    ONC_LAUNCH((decode_pc_kernel<MODE, kFromLen, kBlkFused, kLine>), dim3(g), dim3(64 * (1 + kPcConsumers)), 0, s, a);
-    return hipGetLastError();
-}
-
-template <bool kLine>
-hipError_t launch_message_decode_pc(const DecArgs& a, int mode, hipStream_t s) {
-    if (a.rec_len) {
-        const bool fused = a.blk_base == nullptr;
-        if (mode == ONC_DECODE_BYTES)
-            return fused ? launch_pc<ONC_DECODE_BYTES, true, true, kLine>(a, s) : launch_pc<ONC_DECODE_BYTES, true, false, kLine>(a, s);
-        return fused ? launch_pc<ONC_DECODE_SLICE, true, true, kLine>(a, s) : launch_pc<ONC_DECODE_SLICE, true, false, kLine>(a, s);
-    }
-    if (mode == ONC_DECODE_BYTES) return launch_pc<ONC_DECODE_BYTES, false, false, kLine>(a, s);
-    return launch_pc<ONC_DECODE_SLICE, false, false, kLine>(a, s);
-}
-
 // dlen_tiles: per 4096-record block (256 threads x 16 lengths) the byte
 // total of every 64-record decode workgroup (4 threads) and of the block.
 __global__ __launch_bounds__(256) void dlen_tiles_kernel(const uint32_t* len, uint64_t n, uint64_t* tile_sum,
@@ -1291,10 +887,6 @@ hipError_t launch_decode(const DecArgs& a, int mode, hipStream_t s) {
             ONC_LAUNCH((decode_kernel<ONC_DECODE_SLICE, true, true, false, false, true>), dim3(uint32_t(tiles)),
                        dim3(kDecTile), 0, s, a);
         return hipGetLastError();
-    }
-    if (a.variant & ONC_VARIANT_DEC_PC) {           // (lab: the producer/consumer decode)
-        if (a.line) return launch_message_decode_pc<true>(a, mode, s);
-        return launch_message_decode_pc<false>(a, mode, s);
     }
     if (a.line) return launch_message_decode<true>(a, mode, s);
     return launch_message_decode<false>(a, mode, s);

@@ -2,9 +2,12 @@
 # Round-6 GPU steps (one call runs several; every GPU step has its own
 # timeout; the script stops at the first crash, abort or timeout):
 #   first     the GPU suite, then (suite passed or only failed tests) the
-#             look-back diagnosis and link labs, then (suite green) the
-#             producer/consumer decode A/B (scripts/ab.sh)
-#   ab        the decode A/B only (WLS, ROUNDS)
+#             look-back diagnosis and link labs
+#   sqlds     LDS counters of one workload's kernels
+#   8rank     the driver's 8-GPU command with 8 ranks on this one GPU
+# (The producer/consumer decode A/B and its SQ passes — steps `ab` and
+# `sqpc` with variant 0x80000 — ran against commit 283d487, which still had
+# that lab kernel: profiles/lab_r06_decode_pc_ab.log, sq_r06_decode_pc.json.)
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -18,9 +21,7 @@ case $step in
     crash $rc && exit $rc
     timeout -k 10 120 tools/lookback_diag > gpurun_out/lookback_diag.log 2>&1; r=$?; echo "diag rc=$r"; crash $r && exit $r
     timeout -k 10 180 tools/link_lab > gpurun_out/link_lab.log 2>&1; r=$?; echo "link rc=$r"; crash $r && exit $r
-    [ $rc -eq 0 ] || exit $rc
-    CASES="prod:onc-rpc_amd/libonc_rpc_amd.so:0 pc:onc-rpc_amd/libonc_rpc_amd.so:0x80000" WLS="${WLS:-c1 c0 c2 c3}" \
-      ROUNDS=${ROUNDS:-2} TESTS=0 bash scripts/ab.sh > gpurun_out/ab_pc.log 2>&1; r=$?; cat gpurun_out/ab_pc.log; exit $r ;;
+    exit $rc ;;
   sqlds)
     # LDS counters of the configs[0] encode: one --pmc pass, kernel trace only
     wl=${1:-c0}
@@ -41,24 +42,4 @@ case $step in
       > gpurun_out/bench_8ranks_same_device.log 2>&1; r=$?
     kill $hb 2>/dev/null
     echo "8 ranks rc=$r wall_s=$(( $(date +%s) - s0 ))" | tee -a gpurun_out/bench_8ranks_same_device.log; exit $r ;;
-  sqpc)
-    # SQ counters of the product decode and the producer/consumer decode (two --pmc passes each)
-    OUT=$PWD/gpurun_out
-    P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_WAIT_ANY"
-    P2="SQ_WAVES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS"
-    for wl in ${WLS:-c1 c0}; do for v in 0 0x80000; do
-      i=0
-      for grp in "$P1" "$P2"; do
-        i=$((i+1))
-        timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $grp -d $OUT/sqpc_${wl}_${v}_$i -o run --output-format csv -- \
-          python3 bench.py --workload $wl --variant $v --steps 3 --warmup 1 --no-cpu-baseline --no-pcie --c4-leg off \
-          --iov-leg off --cache-leg off > $OUT/sqpc_${wl}_${v}_$i.log 2>&1
-        r=$?; echo "sqpc $wl $v pass $i rc=$r"; [ $r -eq 0 ] || exit $r
-      done
-      python3 scripts/sq_json.py $OUT/sqpc_${wl}_$v.json "rocprofv3 --kernel-trace --pmc, 2 passes, bench.py --workload $wl --variant $v --steps 3 --warmup 1" \
-        $(ls $OUT/sqpc_${wl}_${v}_1/*counter_collection.csv) $(ls $OUT/sqpc_${wl}_${v}_2/*counter_collection.csv) | grep -i decode
-    done; done ;;
-  ab)
-    CASES="prod:onc-rpc_amd/libonc_rpc_amd.so:0 pc:onc-rpc_amd/libonc_rpc_amd.so:0x80000" WLS="${WLS:-c1 c0 c2 c3}" \
-      ROUNDS=${ROUNDS:-2} TESTS=0 bash scripts/ab.sh > gpurun_out/ab_pc.log 2>&1; r=$?; cat gpurun_out/ab_pc.log; exit $r ;;
 esac

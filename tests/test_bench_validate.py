@@ -116,15 +116,56 @@ def test_iov_gather_ok_rebuilds_the_wire(oracle):
     assert bm.iov_gather_ok(hdr, ec, pay, ref[w0:w1])
 
 
-def test_parsed_lines_bytes():
-    """The line count of the zero-copy decode's note: records of 300 bytes
-    packed from 0 — a record's first 48 bytes span two 128-byte lines when
-    they cross a line boundary."""
+def _granules_loop(wire, lens, line):
+    """decode.hip stage_window's granule count, one record at a time."""
+    out, s = [], 0
+    be = lambda o: int.from_bytes(bytes(wire[o:o + 4]), "big")  # noqa: E731
+    pad = lambda x: (4 - x % 4) % 4  # noqa: E731
+    for L in (int(x) for x in lens):
+        q0 = s & 15
+        avail = min(10, (q0 + L + 15) >> 4)
+        r44 = min(4, (q0 + min(L, 44) + 15) >> 4)
+        if line:
+            win = s - q0
+            nch = min(min(8, max(r44, (((win | 127) + 1) - win) >> 4, (q0 + min(L, 128) + 15) >> 4)), avail)
+        else:
+            nch = min(r44, avail)
+        need = min(L, 160)
+        if L >= 36 and 16 * nch >= q0 + 36:
+            mt = be(s + 8)
+            if mt == 0:
+                cl = be(s + 32)
+                vpos = 36 + cl + pad(cl) + 4
+                if cl > 200:
+                    need = 36
+                elif q0 + vpos + 4 <= 16 * nch and vpos + 4 <= L:
+                    vl = be(s + vpos)
+                    need = vpos + 4 + (vl + pad(vl) if vl <= 200 else 0)
+                else:
+                    need = vpos + 4 + 16
+            elif mt == 1:
+                vl = be(s + 20)
+                need = 24 + vl + pad(vl) + 12 if vl <= 200 else 24
+        out.append(max(nch, min(avail, (q0 + need + 15) >> 4)) if L else 0)
+        s += L
+    return out
+
+
+@pytest.mark.parametrize("line", [False, True])
+def test_decode_granules(oracle, line):
+    """bench.decode_granules (the zero-copy leg's h2d request count) agrees
+    with a per-record restatement of stage_window on a mixed Call/Reply wire
+    with AUTH_UNIX credentials, short records and unaligned starts."""
     bm = _bench()
-    lens = np.full(8, 300, np.int64)
-    starts = np.arange(8) * 300
-    want = sum(((s + 47) // 128 - s // 128 + 1) * 128 for s in starts)
-    assert bm.parsed_lines_bytes(lens) == want
+    hb = S.mixed(2000, seed=7, pmin=0, pmax=300)
+    wire, off, st, rec_len = oracle.encode_batch(hb)
+    assert not st.any()
+    w = np.frombuffer(bytes(wire), np.uint8)[:int(off[-1])].copy()
+    lens = rec_len.astype(np.int64)
+    got = bm.decode_granules(w, lens, line=line)
+    want = _granules_loop(w, lens, line)
+    assert got.tolist() == want
+    assert got.min() >= 1 and got.max() <= 10
 
 
 def test_reduce_leg_and_best():

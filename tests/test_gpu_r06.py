@@ -378,74 +378,3 @@ def test_small_batch_lds_placement(codec, R, oracle, n):
         assert out[5:5 + total].cpu().numpy().tobytes() == o_wire
         assert np.array_equal(off.cpu().numpy().view(np.uint64), o_off)
         assert np.array_equal(st.cpu().numpy()[:hb.n], o_st)
-
-
-# ---------------------------------------------------------------------------
-# the producer/consumer decode (lab variant ONC_VARIANT_DEC_PC): bit-exact
-# ---------------------------------------------------------------------------
-DEC_PC = 0x80000
-
-
-def _pc_batches():
-    return [
-        ("mixed_exotic", S.mixed(9000, seed=111, pmin=0, pmax=700, exotic=0.2)),
-        ("random", L.build_batch(S.random_messages(3000, seed=112, max_payload=300))),
-        ("unix16", S.call_unix16(4100, 64, seed=113)),
-        ("c1_shape", S.call_none(70_001, 256, seed=114)),
-        ("c2_shape", S.mixed(40_000, seed=115)),
-        ("ring_wrap", S.call_none(300_000, 40, seed=116)),     # ~9 tiles per workgroup: the ring wraps
-    ]
-
-
-@pytest.fixture(scope="module", params=["standard", "line"])
-def pc_codec(request, R):
-    import torch
-    assert torch.cuda.is_available(), "GPU tests need an MI355X"
-    c = R.Codec(0, variant=DEC_PC,
-                decode_policy=R.DECODE_POLICY_LINE if request.param == "line" else R.DECODE_POLICY_STANDARD)
-    yield c
-    c.close()
-
-
-@pytest.mark.parametrize("mode", [L.DECODE_SLICE, L.DECODE_BYTES])
-def test_pc_decode_golden_and_corrupted(pc_codec, R, oracle, golden, mode):
-    """Golden records (back to back: aligned and misaligned starts) and a
-    corrupted batch: the oracle's statuses, aux words, descriptors and
-    slots, from offsets and from lengths."""
-    recs, _ = all_golden_records(golden)
-    wire, off = L.records_from_wire(recs + recs[::-1] + recs)
-    w = np.concatenate([wire, np.zeros(16, np.uint8)])
-    assert_decoded_equal(R.decode_host_wire(pc_codec, w, off, mode), oracle.decode_batch(w, off, mode), "golden")
-    hb = L.build_batch(S.random_messages(5000, seed=117, max_payload=300))
-    ow, oo, _, _ = oracle.encode_batch(hb)
-    cw, coff = S.corrupt(np.frombuffer(ow + b"\0" * 16, np.uint8), oo, frac=0.6, seed=118 + mode)
-    assert_decoded_equal(R.decode_host_wire(pc_codec, cw, coff, mode), oracle.decode_batch(cw, coff, mode),
-                         "corrupted")
-
-
-@pytest.mark.parametrize("mode", [L.DECODE_SLICE, L.DECODE_BYTES])
-@pytest.mark.parametrize("name", [b[0] for b in _pc_batches()])
-def test_pc_decode_batches(pc_codec, R, oracle, mode, name):
-    """Configs-shaped and mixed batches through onc_decode and
-    onc_decode_lengths (block totals summed in the kernel, and scanned by a
-    separate launch): equal to the oracle and to the product decode."""
-    import torch
-    hb = dict(_pc_batches())[name]
-    w, off, st, _ = oracle.encode_batch(hb)
-    wire = np.frombuffer(w + b"\0" * 16, np.uint8)
-    ora = oracle.decode_batch(wire, off, mode)
-    assert_decoded_equal(R.decode_host_wire(pc_codec, wire, off, mode), ora, name + " offsets")
-    from test_gpu_decode_lengths import _decode_lengths
-    lens = np.diff(off.astype(np.int64)).astype(np.uint32)
-    got, goff = _decode_lengths(R, pc_codec, w, lens, 0, mode)
-    assert_decoded_equal(got, ora, name + " lengths")
-    assert np.array_equal(goff, off.astype(np.uint64))
-    c2 = R.Codec(0, variant=DEC_PC, force_scan=True)
-    try:
-        got, goff = _decode_lengths(R, c2, b"\0" * 5 + w, lens, 5, mode)
-        assert np.array_equal(goff, off.astype(np.uint64) + 5)
-        ora5 = oracle.decode_batch(np.concatenate([np.zeros(5, np.uint8), wire]), off + 5, mode)
-        assert_decoded_equal(got, ora5, name + " lengths, scanned block totals, base 5")
-    finally:
-        c2.close()
-    torch.cuda.empty_cache()
