@@ -290,6 +290,10 @@ struct ImgSink {
     }
 };
 
+#ifndef ONC_UNIX_PF
+#define ONC_UNIX_PF 1
+#endif
+
 #if defined(ONC_LAB_HDR)
 struct XorSink {
     uint32_t acc;
@@ -663,6 +667,22 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     }
     if constexpr (kLen) asm volatile("" : "+v"(glen));
     const onc_msg dm = as_msg(mr);
+#if ONC_UNIX_PF
+    // The two lines of the lane's AUTH_UNIX credential block touched now, so
+    // that the header build's block loads (span 2's above all, which wait
+    // behind span 1's stores) hit L2 instead of HBM: enc_len reads declared
+    // lengths and never touches the table. Results unused (kept live to the
+    // tile's end: no wait is placed for them).
+    uint32_t pf0 = 0, pf1 = 0;
+    if constexpr (!kRoot && !kGiven && !kSmall) {        // (the wave-per-tile kernel: in the others it spills)
+        const bool pu = lane < nrec && dm.msg_type == ONC_MSG_CALL && (dm.cred.kind_len >> 24) == ONC_KIND_UNIX &&
+                        dm.cred.ref < a.bounds.n_unix;
+        const uintptr_t ub = pu ? reinterpret_cast<uintptr_t>(a.unix + dm.cred.ref)
+                                : reinterpret_cast<uintptr_t>(a.msgs);
+        pf0 = gload<uint32_t>(ub);
+        pf1 = gload<uint32_t>(pu ? ub + sizeof(onc_unix_params) - 4 : ub);
+    }
+#endif
     // output coordinates: byte 0 = the 16-aligned chunk base below the
     // caller's `out`, which sits at `origin` (any writer position)
     uint64_t T0 = 0;
@@ -787,12 +807,23 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
                 // lab builds only (tools/hdr_lab.sh; wrong output bytes):
                 // 1 = no header build at all (the image stays zero),
                 // 2 = the header words computed (every load) but not written
-                // to the image: what the LDS writes of the build cost
+                // to the image: what the LDS writes of the build cost,
+                // 3 = everything but the credential block's load
                 if constexpr (ONC_LAB_HDR == 2) {
                     XorSink xs{0u};
                     if (kRoot) put_root_words(d, uint32_t(len), src, a.root, xs);
                     else put_header_words(d, uint32_t(len), src, xs, nullptr, false, &dc);
                     if (xs.acc == 0x9E3779B9u) img32[0] = xs.acc;       // keeps the words live
+                } else if constexpr (ONC_LAB_HDR == 3) {
+                    // 3 = the header written with a register-made credential
+                    // block (stamp 0, uid 501, gid 20, 16 gids, no name): the
+                    // whole build but the block's load
+                    UnixRegs fk;
+                    fk.q[0] = u32x4{0u, 501u, 20u, 16u};
+                    fk.q[1] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+                    for (int k = 2; k < 6; ++k) fk.q[k] = u32x4{uint32_t(k), 7u, 11u, 13u};
+                    put_header_words(d, uint32_t(len), src, w, &fk, true, &dc);
                 }
 #else
                 if (kRoot) put_root_words(d, uint32_t(len), src, a.root, w);
@@ -848,6 +879,9 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         if (lo_rec == hi_rec && hi_rec == nrec) ONC_PROF(4);
     }
     ONC_PROF(5);
+#if ONC_UNIX_PF
+    asm volatile("" ::"v"(pf0), "v"(pf1));
+#endif
 }
 
 // ---------------------------------------------------------------------------
