@@ -699,7 +699,10 @@ def c2_zero_copy_variants(args, torch, R, codec, w, rl, o, n, n_total, total_byt
       step pins it (onc_host_register of the 1.9 GB wire and of its lengths),
       decodes it in place, synchronises and unpins it; host wall clock (the
       registration is synchronous host work). The data is written into the
-      buffer before the timed loop (the pages are resident, as after a recv).
+      buffer before the timed calls (the pages are resident, as after a recv).
+      A fresh buffer pair per batch (register_per_batch) and the same pair
+      every batch (register_per_batch_recycled) are timed apart: the runtime
+      re-pins a range it has pinned before far faster.
     policy_standard / policy_line / policy_auto — the same registered-once
       decode under each first-round policy pinned (onc_codec_set_decode_policy):
       STANDARD fetches each record's first 44 bytes (a 64-byte span), LINE the
@@ -733,44 +736,69 @@ def c2_zero_copy_variants(args, torch, R, codec, w, rl, o, n, n_total, total_byt
         def data_ptr(self):
             return self.p
 
-    def one(fresh):
+    def make_pair():
         mm = mmap.mmap(-1, total_bytes + 16 + 4096)
         mm_l = mmap.mmap(-1, 4 * n + 4096)
-        hb_w = hb_l = None
-        try:
-            hb_w = np.frombuffer(mm, np.uint8, count=total_bytes + 16)
-            hb_w[:] = w.host[:total_bytes + 16]
-            hb_l = np.frombuffer(mm_l, np.uint8, count=4 * n)
-            hb_l[:] = rl.host[:4 * n]
-            aw, al = hb_w.ctypes.data, hb_l.ctypes.data
-            dw, dl = C.c_void_p(), C.c_void_p()
-            t0 = time.perf_counter()
-            codec._check(lib.onc_host_register(codec.h, C.c_void_p(aw), total_bytes + 16, C.byref(dw)), "register")
-            codec._check(lib.onc_host_register(codec.h, C.c_void_p(al), 4 * n, C.byref(dl)), "register")
-            t1 = time.perf_counter()
-            codec.decode_lengths(_Dev(dw.value), _Dev(dl.value), n, 0, mode, o.msgs, o.unix, o.status, o.aux0,
-                                 o.aux1, rec_off=o.off)
-            codec.sync()
-            t2 = time.perf_counter()
-            codec._check(lib.onc_host_unregister(codec.h, C.c_void_p(aw)), "unregister")
-            codec._check(lib.onc_host_unregister(codec.h, C.c_void_p(al)), "unregister")
-            t3 = time.perf_counter()
-            return (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3
-        finally:
-            del hb_w, hb_l
-            mm.close()
-            mm_l.close()
-    one(True)
+        hb_w = np.frombuffer(mm, np.uint8, count=total_bytes + 16)
+        hb_w[:] = w.host[:total_bytes + 16]
+        hb_l = np.frombuffer(mm_l, np.uint8, count=4 * n)
+        hb_l[:] = rl.host[:4 * n]
+        return mm, mm_l, hb_w, hb_l
+
+    def one(pair):
+        _, _, hb_w, hb_l = pair
+        aw, al = hb_w.ctypes.data, hb_l.ctypes.data
+        dw, dl = C.c_void_p(), C.c_void_p()
+        t0 = time.perf_counter()
+        codec._check(lib.onc_host_register(codec.h, C.c_void_p(aw), total_bytes + 16, C.byref(dw)), "register")
+        codec._check(lib.onc_host_register(codec.h, C.c_void_p(al), 4 * n, C.byref(dl)), "register")
+        t1 = time.perf_counter()
+        codec.decode_lengths(_Dev(dw.value), _Dev(dl.value), n, 0, mode, o.msgs, o.unix, o.status, o.aux0,
+                             o.aux1, rec_off=o.off)
+        codec.sync()
+        t2 = time.perf_counter()
+        codec._check(lib.onc_host_unregister(codec.h, C.c_void_p(aw)), "unregister")
+        codec._check(lib.onc_host_unregister(codec.h, C.c_void_p(al)), "unregister")
+        t3 = time.perf_counter()
+        return (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3
+
+    def close(pair):
+        mm, mm_l, hb_w, hb_l = pair
+        del hb_w, hb_l, pair
+        mm.close()
+        mm_l.close()
+
+    def leg(parts, r, note):
+        reg, dec, unreg = (float(x) for x in np.array(parts).mean(axis=0))
+        ms = reg + dec + unreg
+        return {"value": n_total / (ms / 1e3) / 1e6, "ms_per_step": ms, "validated": check_dec(),
+                "register_ms": reg, "decode_sync_ms": dec, "unregister_ms": unreg, "batches": r, "note": note}
     r = max(2, min(reps, 4))
-    parts = np.array([one(True) for _ in range(r)])
-    reg, dec, unreg = (float(x) for x in parts.mean(axis=0))
-    ms = reg + dec + unreg
-    out["register_per_batch"] = {
-        "value": n_total / (ms / 1e3) / 1e6, "ms_per_step": ms, "validated": check_dec(),
-        "register_ms": reg, "decode_sync_ms": dec, "unregister_ms": unreg, "batches": r,
-        "note": f"a fresh unpinned buffer pair per batch (pages already written, as after a recv): "
-                f"onc_host_register of the {total_bytes}-byte wire + its lengths, the in-place decode and a "
-                "synchronisation, onc_host_unregister (host wall clock of each call, mean over batches)"}
+    # fresh: a new buffer pair per batch (never registered before)
+    parts = []
+    for k in range(r + 1):
+        pair = make_pair()
+        try:
+            t = one(pair)
+        finally:
+            close(pair)
+        if k:
+            parts.append(t)
+    out["register_per_batch"] = leg(parts, r,
+        f"a fresh unpinned buffer pair per batch (pages already written, as after a recv): onc_host_register of "
+        f"the {total_bytes}-byte wire + its lengths, the in-place decode and a synchronisation, "
+        "onc_host_unregister (host wall clock of each call, mean over batches)")
+    # recycled: the same buffer pair registered and unregistered every batch
+    # (a server recycling its receive buffers without keeping them pinned)
+    pair = make_pair()
+    try:
+        one(pair)
+        parts = [one(pair) for _ in range(r)]
+    finally:
+        close(pair)
+    out["register_per_batch_recycled"] = leg(parts, r,
+        "the same unpinned buffer pair registered, decoded in place and unregistered every batch "
+        "(host wall clock of each call, mean over batches)")
     return out
 
 
@@ -1584,7 +1612,8 @@ def run_main(args, torch, R, S, SH, L, dist, rank, world, local_rank, mode):
                             n_total, bool((kinds == L.KIND_UNIX).any()))
         if wl == "c2":
             zc = reduce_leg(torch, dist, dev, zc, [""] + ([] if args.frame else [
-                "variants.register_per_batch", "variants.policy_standard", "variants.policy_line",
+                "variants.register_per_batch", "variants.register_per_batch_recycled", "variants.policy_standard",
+                "variants.policy_line",
                 "variants.policy_auto"]), n_total)
         else:
             zc.setdefault("variants", {})

@@ -290,10 +290,6 @@ struct ImgSink {
     }
 };
 
-#ifndef ONC_UNIX_PF
-#define ONC_UNIX_PF 1
-#endif
-
 #if defined(ONC_LAB_HDR)
 struct XorSink {
     uint32_t acc;
@@ -667,22 +663,6 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
     }
     if constexpr (kLen) asm volatile("" : "+v"(glen));
     const onc_msg dm = as_msg(mr);
-#if ONC_UNIX_PF
-    // The two lines of the lane's AUTH_UNIX credential block touched now, so
-    // that the header build's block loads (span 2's above all, which wait
-    // behind span 1's stores) hit L2 instead of HBM: enc_len reads declared
-    // lengths and never touches the table. Results unused (kept live to the
-    // tile's end: no wait is placed for them).
-    uint32_t pf0 = 0, pf1 = 0;
-    if constexpr (!kRoot && !kGiven && !kSmall) {        // (the wave-per-tile kernel: in the others it spills)
-        const bool pu = lane < nrec && dm.msg_type == ONC_MSG_CALL && (dm.cred.kind_len >> 24) == ONC_KIND_UNIX &&
-                        dm.cred.ref < a.bounds.n_unix;
-        const uintptr_t ub = pu ? reinterpret_cast<uintptr_t>(a.unix + dm.cred.ref)
-                                : reinterpret_cast<uintptr_t>(a.msgs);
-        pf0 = gload<uint32_t>(ub);
-        pf1 = gload<uint32_t>(pu ? ub + sizeof(onc_unix_params) - 4 : ub);
-    }
-#endif
     // output coordinates: byte 0 = the 16-aligned chunk base below the
     // caller's `out`, which sits at `origin` (any writer position)
     uint64_t T0 = 0;
@@ -879,9 +859,6 @@ __device__ __forceinline__ void enc_emit_tile(const EncArgs& a, ImgTile& T, uint
         if (lo_rec == hi_rec && hi_rec == nrec) ONC_PROF(4);
     }
     ONC_PROF(5);
-#if ONC_UNIX_PF
-    asm volatile("" ::"v"(pf0), "v"(pf1));
-#endif
 }
 
 // ---------------------------------------------------------------------------

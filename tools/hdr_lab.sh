@@ -5,7 +5,7 @@
 # wrong by construction; they are timed only (scripts/ab.sh LAB=1).
 set -e
 cd "$(dirname "$0")/../onc-rpc_amd/csrc"
-for v in 1 2 3; do   # (round-6 A/B: the =3 build also had -DONC_UNIX_PF=0)
+for v in 1 2 3; do
   make -s -j8 OBJDIR=../../tools/lab_hdr$v/obj OUT=../../tools/lab_hdr$v/libonc_rpc_amd.so \
     HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -DONC_LAB_HDR=$v"
 done
