@@ -737,17 +737,17 @@ def c2_zero_copy_variants(args, torch, R, codec, w, rl, o, n, n_total, total_byt
             return self.p
 
     def make_pair():
-        mm = mmap.mmap(-1, total_bytes + 16 + 4096)
-        mm_l = mmap.mmap(-1, 4 * n + 4096)
-        hb_w = np.frombuffer(mm, np.uint8, count=total_bytes + 16)
+        # {"mm": mmaps, "a": numpy views, "p": their addresses}; close()
+        # drops the views before unmapping (an exported buffer cannot close)
+        mm = (mmap.mmap(-1, total_bytes + 16 + 4096), mmap.mmap(-1, 4 * n + 4096))
+        hb_w = np.frombuffer(mm[0], np.uint8, count=total_bytes + 16)
         hb_w[:] = w.host[:total_bytes + 16]
-        hb_l = np.frombuffer(mm_l, np.uint8, count=4 * n)
+        hb_l = np.frombuffer(mm[1], np.uint8, count=4 * n)
         hb_l[:] = rl.host[:4 * n]
-        return mm, mm_l, hb_w, hb_l
+        return {"mm": mm, "a": [hb_w, hb_l], "p": (hb_w.ctypes.data, hb_l.ctypes.data)}
 
     def one(pair):
-        _, _, hb_w, hb_l = pair
-        aw, al = hb_w.ctypes.data, hb_l.ctypes.data
+        aw, al = pair["p"]
         dw, dl = C.c_void_p(), C.c_void_p()
         t0 = time.perf_counter()
         codec._check(lib.onc_host_register(codec.h, C.c_void_p(aw), total_bytes + 16, C.byref(dw)), "register")
@@ -763,10 +763,9 @@ def c2_zero_copy_variants(args, torch, R, codec, w, rl, o, n, n_total, total_byt
         return (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3
 
     def close(pair):
-        mm, mm_l, hb_w, hb_l = pair
-        del hb_w, hb_l, pair
-        mm.close()
-        mm_l.close()
+        pair["a"].clear()
+        for m in pair["mm"]:
+            m.close()
 
     def leg(parts, r, note):
         reg, dec, unreg = (float(x) for x in np.array(parts).mean(axis=0))
