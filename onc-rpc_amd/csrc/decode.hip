@@ -30,6 +30,9 @@ namespace onc {
 #ifndef ONC_DEC_WIN
 #define ONC_DEC_WIN 10
 #endif
+#ifndef ONC_DEC_BUF
+#define ONC_DEC_BUF 1       // round 1 through a buffer resource (stage_window)
+#endif
 constexpr uint32_t kWin1 = 4;                 // round-1 chunks (standard policy)
 constexpr uint32_t kWin1L = 8;                // round-1 chunks at most (line policy, decode_kernel)
 constexpr uint32_t kWinChunks = ONC_DEC_WIN;
@@ -541,12 +544,42 @@ __device__ __forceinline__ uint32_t stage_window(uint32_t* s_win, int t, uintptr
     // branches the compiler waited for chunk 2 before issuing chunk 3
     u32x4 v[kWin1L];
     const uintptr_t last = win + 16 * (nch - 1);          // nch >= 1 here (L != 0)
+    static_assert(kWin1 == 4 && kWin1L == 8, "pin lists below");
+#if ONC_DEC_BUF
+    // Round 1 through a buffer resource based at the first active lane's
+    // window when every active lane's window lies within 2 GiB above it
+    // (records back to back: always, short of multi-GiB records): a chunk
+    // past the record's round is given an out-of-range offset, so its load
+    // returns zeros without a memory request — instead of re-reading the
+    // record's last granule, a second request for the same bytes (on a
+    // mapped host wire each one crosses the link: tools/link_lab.hip).
+    const uintptr_t rb = __builtin_amdgcn_readfirstlane(uint32_t(win)) |
+                         (uintptr_t(__builtin_amdgcn_readfirstlane(uint32_t(win >> 32))) << 32);
+    const bool near = win >= rb && win - rb < (uintptr_t(1) << 31) - 256;
+    if (__ballot(!near) == 0) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void*>(rb), int16_t(0), int32_t(0x7FFFFFF0), int32_t(0x00020000));
+        const uint32_t wo = uint32_t(win - rb);
+#pragma unroll
+        for (uint32_t j = 0; j < kWin1L; ++j) {
+            if (j < kWin1 || kLine)
+                v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rs, j < nch ? wo + 16 * j : 0x80000000u, 0, 0));
+        }
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < kWin1L; ++j)
+            if (j < kWin1 || kLine) v[j] = gload<u32x4>(min(win + 16 * j, last));
+    }
+#else
 #pragma unroll
     for (uint32_t j = 0; j < kWin1; ++j) v[j] = gload<u32x4>(min(win + 16 * j, last));
-    static_assert(kWin1 == 4 && kWin1L == 8, "pin lists below");
     if constexpr (kLine) {
 #pragma unroll
         for (uint32_t j = kWin1; j < kWin1L; ++j) v[j] = gload<u32x4>(min(win + 16 * j, last));
+    }
+#endif
+    if constexpr (kLine) {
         asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
                      "+v"(v[7]));
     } else {

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-6 A/B of the decode's round-1 buffer loads (the library, ONC_DEC_BUF=1)
+# against the clamped re-reads (tools/lab_nobuf, -DONC_DEC_BUF=0): decode
+# parity suites on the library first, then HBM-resident steps (scripts/ab.sh)
+# and the configs[2] zero-copy decode of a mapped wire with each library.
+set -u
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_decode_lengths.py tests/test_gpu_r04.py \
+  tests/test_gpu_r05.py tests/test_body_roots.py -m gpu -x -q --timeout 200 --timeout-method thread \
+  > gpurun_out/buf_tests.log 2>&1; r=$?; tail -2 gpurun_out/buf_tests.log; [ $r -eq 0 ] || exit $r
+CASES="buf:onc-rpc_amd/libonc_rpc_amd.so:0 nobuf:tools/lab_nobuf/libonc_rpc_amd.so:0" WLS="c1 c2 c0 c3" ROUNDS=2 \
+  bash scripts/ab.sh > gpurun_out/ab_buf.log 2>&1; r=$?; cat gpurun_out/ab_buf.log; [ $r -eq 0 ] || exit $r
+for r in 1 2; do for cs in buf:onc-rpc_amd nobuf:tools/lab_nobuf; do
+  IFS=: read -r name dir <<< "$cs"
+  ONC_RPC_AMD_LIB=$PWD/$dir/libonc_rpc_amd.so timeout -k 10 300 python -u bench.py --workload c2 --c4-leg off \
+    --no-cpu-baseline > gpurun_out/zc_${name}_r$r.log 2>&1 || exit $?
+  python3 -c "import json,sys;d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]);z=d['pcie_inclusive']['zero_copy'];print(sys.argv[1].split('/')[-1], round(z['value'],1), round(z['ms_per_step'],3), {k:round(v['ms_per_step'],3) for k,v in z['variants'].items() if k.startswith('policy')})" gpurun_out/zc_${name}_r$r.log
+done; done

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                                  \
@@ -47,11 +48,42 @@ __global__ __launch_bounds__(256) void scatter_read(const uint8_t* base, uint64_
     if (acc == 0x9E3779B9u) sink[0] = acc;             // (keeps the loads)
 }
 
-int main() {
+// kLoads dwordx4 loads per lane of which only the first `nd` granules are
+// distinct: loads past them re-read the last one (the decode's round-1
+// pattern, clamped to the record's last granule): do the re-reads cross
+// the link again?
+template <int kLoads>
+__global__ __launch_bounds__(256) void clamp_read(const uint8_t* base, uint64_t n, uint64_t stride, uint32_t nd,
+                                                  uint32_t* sink) {
+    const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    uint32_t acc = 0;
+    if (i < n) {
+        const uint8_t* p = base + i * stride;
+        u32x4 v[kLoads];
+#pragma unroll
+        for (int k = 0; k < kLoads; ++k)
+            v[k] = *reinterpret_cast<const u32x4*>(p + 16 * (uint32_t(k) < nd ? k : nd - 1));
+#pragma unroll
+        for (int k = 0; k < kLoads; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+int main(int argc, char** argv) {
     setvbuf(stdout, nullptr, _IONBF, 0);
     const uint64_t kMax = (1ull << 30) * 9 / 4;          // 2.25 GiB of mapped host memory
+    // "reg": plain pages registered with hipHostRegister (what
+    // onc_host_register does to a socket buffer) instead of hipHostMalloc
+    const bool reg = argc > 1 && std::string(argv[1]) == "reg";
     uint8_t* h = nullptr;
-    CK(hipHostMalloc(reinterpret_cast<void**>(&h), kMax, hipHostMallocMapped));
+    if (reg) {
+        h = static_cast<uint8_t*>(std::aligned_alloc(4096, kMax));
+        if (!h) return 1;
+        CK(hipHostRegister(h, kMax, hipHostRegisterMapped | hipHostRegisterPortable));
+    } else {
+        CK(hipHostMalloc(reinterpret_cast<void**>(&h), kMax, hipHostMallocMapped));
+    }
+    printf("# memory: %s\n", reg ? "aligned_alloc + hipHostRegister" : "hipHostMalloc");
     for (uint64_t k = 0; k < kMax; k += 4096) h[k] = uint8_t(k >> 12);
     uint8_t* d = nullptr;
     CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0));
@@ -99,6 +131,30 @@ int main() {
                c.n * c.bytes / us / 1e3, c.n * 64.0 * ((c.bytes + 63) / 64) / us / 1e3,
                c.n * 128.0 * ((c.bytes + 127) / 128) / us / 1e3);
     }
-    CK(hipHostFree(h));
+    // re-reads: 4 loads per record, 1..4 distinct granules (stride 1936)
+    printf("# clamped re-reads: 4 dwordx4 loads per lane at stride 1936, `distinct` of them distinct granules\n");
+    for (uint32_t nd = 1; nd <= 4; ++nd) {
+        std::vector<float> t;
+        const uint64_t n = uint64_t(1) << 20;
+        for (int rep = 0; rep < 6; ++rep) {
+            CK(hipEventRecord(e0, 0));
+            hipLaunchKernelGGL(clamp_read<4>, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, 0, d, n, uint64_t(1936),
+                               nd, sink);
+            CK(hipGetLastError());
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (rep) t.push_back(ms);
+        }
+        std::sort(t.begin(), t.end());
+        printf("loads 4 distinct %u: %10.1f us\n", nd, t[t.size() / 2] * 1e3);
+    }
+    if (reg) {
+        CK(hipHostUnregister(h));
+        std::free(h);
+    } else {
+        CK(hipHostFree(h));
+    }
     return 0;
 }
