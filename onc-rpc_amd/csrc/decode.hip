@@ -556,10 +556,11 @@ __device__ __forceinline__ uint32_t stage_window(uint32_t* s_win, int t, uintptr
     const uintptr_t rb = __builtin_amdgcn_readfirstlane(uint32_t(win)) |
                          (uintptr_t(__builtin_amdgcn_readfirstlane(uint32_t(win >> 32))) << 32);
     const bool near = win >= rb && win - rb < (uintptr_t(1) << 31) - 256;
-    if (__ballot(!near) == 0) {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<void*>(rb), int16_t(0), int32_t(0x7FFFFFF0), int32_t(0x00020000));
-        const uint32_t wo = uint32_t(win - rb);
+    const bool use_buf = __ballot(!near) == 0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(rb), int16_t(0), int32_t(0x7FFFFFF0), int32_t(0x00020000));
+    const uint32_t wo = uint32_t(win - rb);
+    if (use_buf) {
 #pragma unroll
         for (uint32_t j = 0; j < kWin1L; ++j) {
             if (j < kWin1 || kLine)
