@@ -69,6 +69,21 @@ __global__ __launch_bounds__(256) void clamp_read(const uint8_t* base, uint64_t 
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// The same bytes read cooperatively: kGran lanes per record, lane g of a
+// record loading its granule g — one instruction covers 64 / kGran records'
+// contiguous 16 * kGran bytes each (does the link see fewer requests?)
+template <int kGran>
+__global__ __launch_bounds__(256) void coop_read(const uint8_t* base, uint64_t n, uint64_t stride, uint32_t* sink) {
+    const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    const uint64_t i = t / kGran;
+    uint32_t acc = 0;
+    if (i < n) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(base + i * stride + 16 * (t % kGran));
+        acc = v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 int main(int argc, char** argv) {
     setvbuf(stdout, nullptr, _IONBF, 0);
     const uint64_t kMax = (1ull << 30) * 9 / 4;          // 2.25 GiB of mapped host memory
@@ -149,6 +164,33 @@ int main(int argc, char** argv) {
         }
         std::sort(t.begin(), t.end());
         printf("loads 4 distinct %u: %10.1f us\n", nd, t[t.size() / 2] * 1e3);
+    }
+    // cooperative rows against the per-lane rows above (same bytes per record)
+    printf("# cooperative: kGran lanes per record, one 16-byte granule each (stride 1936 and 300)\n");
+    for (uint64_t stride : {uint64_t(1936), uint64_t(300)}) {
+        for (int g : {1, 2, 3, 4, 8}) {
+            const uint64_t n = uint64_t(1) << 20;
+            std::vector<float> t;
+            for (int rep = 0; rep < 6; ++rep) {
+                const dim3 grid(uint32_t((n * g + 255) / 256));
+                CK(hipEventRecord(e0, 0));
+                switch (g) {
+                    case 1: hipLaunchKernelGGL(coop_read<1>, grid, dim3(256), 0, 0, d, n, stride, sink); break;
+                    case 2: hipLaunchKernelGGL(coop_read<2>, grid, dim3(256), 0, 0, d, n, stride, sink); break;
+                    case 3: hipLaunchKernelGGL(coop_read<3>, grid, dim3(256), 0, 0, d, n, stride, sink); break;
+                    case 4: hipLaunchKernelGGL(coop_read<4>, grid, dim3(256), 0, 0, d, n, stride, sink); break;
+                    default: hipLaunchKernelGGL(coop_read<8>, grid, dim3(256), 0, 0, d, n, stride, sink); break;
+                }
+                CK(hipGetLastError());
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (rep) t.push_back(ms);
+            }
+            std::sort(t.begin(), t.end());
+            printf("coop stride %lu bytes %d: %10.1f us\n", (unsigned long)stride, 16 * g, t[t.size() / 2] * 1e3);
+        }
     }
     if (reg) {
         CK(hipHostUnregister(h));
