@@ -30,8 +30,8 @@ namespace onc {
 #ifndef ONC_DEC_WIN
 #define ONC_DEC_WIN 10
 #endif
-#ifndef ONC_DEC_BUF
-#define ONC_DEC_BUF 1       // round 1 through a buffer resource (stage_window)
+#ifndef ONC_DEC_COOP
+#define ONC_DEC_COOP 1      // round 1 loaded cooperatively (load_round1)
 #endif
 constexpr uint32_t kWin1 = 4;                 // round-1 chunks (standard policy)
 constexpr uint32_t kWin1L = 8;                // round-1 chunks at most (line policy, decode_kernel)
@@ -523,14 +523,14 @@ static_assert(kDecTile == 64, "kFromLen: one wave per workgroup, 64 workgroup to
 // decode 1-2 us of prologue; results never depend on the policy (only which
 // chunks each round loads); onc_codec_set_decode_policy pins either (tests).
 
-// The window of one record (L != 0): round 1, the header extent, round 2.
-// Returns the chunks staged in LDS; needs2: the header reaches past the
-// standard policy's first round. kLine: the line policy (decode_kernel).
-template <bool kLine, bool kPolicy, bool kRoot>
-__device__ __forceinline__ uint32_t stage_window(uint32_t* s_win, int t, uintptr_t base, uintptr_t win, uint32_t q0,
-                                                 uint32_t d0, uint64_t L, bool& needs2) {
-    const uint32_t avail = uint32_t(min(uint64_t(kWinChunks), (q0 + L + 15) >> 4));
-    const uint32_t r44 = kPolicy ? uint32_t(min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4)) : kWin1;
+// Round 1 of a record's window (L != 0): the chunks it takes under the
+// policy. avail: the record's chunks inside the window; r44: the standard
+// round (the first 44 bytes).
+template <bool kLine, bool kPolicy>
+__device__ __forceinline__ uint32_t round1_chunks(uintptr_t win, uint32_t q0, uint64_t L, uint32_t& avail,
+                                                  uint32_t& r44) {
+    avail = uint32_t(min(uint64_t(kWinChunks), (q0 + L + 15) >> 4));
+    r44 = kPolicy ? uint32_t(min(uint64_t(kWin1), (q0 + min(L, uint64_t(44)) + 15) >> 4)) : kWin1;
     // line policy: also the rest of the record's first 128-byte line, and
     // at least the record's first 128 bytes (a record starting inside a line
     // takes the next line in round 1 too: configs[0]'s 128-byte headers 192
@@ -538,56 +538,93 @@ __device__ __forceinline__ uint32_t stage_window(uint32_t* s_win, int t, uintptr
     const uint32_t rln = uint32_t((((win | 127u) + 1u) - win) >> 4);
     const uint32_t r128 = uint32_t((q0 + min(L, uint64_t(128)) + 15) >> 4);
     const uint32_t r1 = kLine ? min(kWin1L, max(max(r44, rln), r128)) : r44;
-    uint32_t nch = min(r1, avail);
-    // all round-1 loads issued without a per-chunk branch (chunks past
-    // the record's last granule re-read that granule) and pinned: under
-    // branches the compiler waited for chunk 2 before issuing chunk 3
-    u32x4 v[kWin1L];
-    const uintptr_t last = win + 16 * (nch - 1);          // nch >= 1 here (L != 0)
+    return min(r1, avail);
+}
+
+// Round 1's loads for the whole wave (every lane, nch = 0 for a lane with no
+// record). They go through a buffer resource based at the first record's
+// window when every window lies within 2 GiB above it (records back to
+// back: always, short of multi-GiB records): a chunk past a record's round
+// gets an out-of-range offset, so its load returns zeros without a memory
+// request (it used to re-read the record's last granule: a second request
+// on a mapped host wire on some hosts, profiles/lab_r06_decode_buffer_round1.log).
+// kCoop: the lanes load the wave's records granule by granule — lane t of
+// instruction k takes granule t % G of record k * (64 / G) + t / G, so one
+// instruction reads 64 / G records' windows contiguously — and hand them
+// over through LDS: over PCIe the link then sees a record's round as one
+// contiguous request rather than G (tools/link_lab.hip coop rows).
+// No branch separates the loads: under branches the compiler waited for
+// chunk 2 before issuing chunk 3.
+template <bool kLine, bool kCoop>
+__device__ __forceinline__ void load_round1(uint32_t* s_win, int t, uintptr_t win, uint32_t nch, u32x4 (&v)[kWin1L]) {
+    constexpr uint32_t G = kLine ? kWin1L : kWin1;
     static_assert(kWin1 == 4 && kWin1L == 8, "pin lists below");
-#if ONC_DEC_BUF
-    // Round 1 through a buffer resource based at the first active lane's
-    // window when every active lane's window lies within 2 GiB above it
-    // (records back to back: always, short of multi-GiB records): a chunk
-    // past the record's round is given an out-of-range offset, so its load
-    // returns zeros without a memory request — instead of re-reading the
-    // record's last granule, a second request for the same bytes (on a
-    // mapped host wire each one crosses the link: tools/link_lab.hip).
-    const uintptr_t rb = __builtin_amdgcn_readfirstlane(uint32_t(win)) |
-                         (uintptr_t(__builtin_amdgcn_readfirstlane(uint32_t(win >> 32))) << 32);
-    const bool near = win >= rb && win - rb < (uintptr_t(1) << 31) - 256;
-    const bool use_buf = __ballot(!near) == 0;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(rb), int16_t(0), int32_t(0x7FFFFFF0), int32_t(0x00020000));
-    const uint32_t wo = uint32_t(win - rb);
-    if (use_buf) {
 #pragma unroll
-        for (uint32_t j = 0; j < kWin1L; ++j) {
-            if (j < kWin1 || kLine)
+    for (uint32_t j = 0; j < kWin1L; ++j) v[j] = u32x4{0u, 0u, 0u, 0u};
+    const uint64_t act = __ballot(nch != 0);
+    if (act == 0) return;
+    const int first = __builtin_ctzll(act);
+    const uintptr_t rb = uintptr_t(__builtin_amdgcn_readlane(uint32_t(win), first)) |
+                         (uintptr_t(__builtin_amdgcn_readlane(uint32_t(win >> 32), first)) << 32);
+    const bool near = nch == 0 || (win >= rb && win - rb < (uintptr_t(1) << 31) - 256);
+    const uint32_t wo = uint32_t(win - rb);
+    if (__ballot(!near) == 0) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void*>(rb), int16_t(0), int32_t(0x7FFFFFF0), int32_t(0x00020000));
+        if constexpr (kCoop) {
+            constexpr uint32_t R = 64 / G;                   // records per instruction
+            u32x4 x[G];
+#pragma unroll
+            for (uint32_t k = 0; k < G; ++k) {
+                const int r = int(k * R + uint32_t(t) / G);
+                const uint32_t g = uint32_t(t) % G;
+                const uint32_t wr = uint32_t(__shfl(int(wo), r));
+                const uint32_t nr = uint32_t(__shfl(int(nch), r));
+                x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rs, g < nr ? wr + 16 * g : 0x80000000u, 0, 0));
+            }
+            // record r's granule g at raw[r * G + g] (the window is free
+            // until staging; one wave per workgroup, LDS in issue order)
+            u32x4* raw = reinterpret_cast<u32x4*>(s_win);
+#pragma unroll
+            for (uint32_t k = 0; k < G; ++k) raw[(k * R + uint32_t(t) / G) * G + uint32_t(t) % G] = x[k];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (uint32_t j = 0; j < G; ++j) v[j] = raw[uint32_t(t) * G + j];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < G; ++j)
                 v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                      rs, j < nch ? wo + 16 * j : 0x80000000u, 0, 0));
         }
-    } else {
+    } else if (nch != 0) {
+        // windows too far apart for one resource: per-lane loads, chunks
+        // past the round re-reading the record's last granule
+        const uintptr_t last = win + 16 * (nch - 1);
 #pragma unroll
-        for (uint32_t j = 0; j < kWin1L; ++j)
-            if (j < kWin1 || kLine) v[j] = gload<u32x4>(min(win + 16 * j, last));
+        for (uint32_t j = 0; j < G; ++j) v[j] = gload<u32x4>(min(win + 16 * j, last));
     }
-#else
-#pragma unroll
-    for (uint32_t j = 0; j < kWin1; ++j) v[j] = gload<u32x4>(min(win + 16 * j, last));
-    if constexpr (kLine) {
-#pragma unroll
-        for (uint32_t j = kWin1; j < kWin1L; ++j) v[j] = gload<u32x4>(min(win + 16 * j, last));
-    }
-#endif
     if constexpr (kLine) {
         asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
                      "+v"(v[7]));
     } else {
         asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
-#pragma unroll
-        for (uint32_t j = kWin1; j < kWin1L; ++j) v[j] = u32x4{0u, 0u, 0u, 0u};
     }
+}
+
+// The window of one record (L != 0), round 1 loaded (v, nch: load_round1):
+// staged, the header extent, round 2. Returns the chunks staged in LDS;
+// needs2: the header reaches past the standard policy's first round. kLine:
+// the line policy (decode_kernel).
+template <bool kLine, bool kPolicy, bool kRoot>
+__device__ __forceinline__ uint32_t stage_window(uint32_t* s_win, int t, uintptr_t base, uintptr_t win, uint32_t q0,
+                                                 uint32_t d0, uint64_t L, bool& needs2, const u32x4 (&v)[kWin1L],
+                                                 uint32_t nch, uint32_t avail, uint32_t r44) {
     // column word c = record bytes [4c, 4c + 4): loaded words d0 + c and
     // d0 + c + 1 funnelled by the record's byte offset in its dword. The
     // last word of the round (its upper bytes in the next chunk) is
@@ -737,9 +774,13 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     const uint32_t d0 = q0 >> 2;                      // record byte 0's dword in its first granule
     // Stage the window. Chunks past the record's last byte are not loaded;
     // empty records read nothing.
-    uint32_t nch = 0;
+    constexpr bool kLineP = kLine && kPolicy;
+    uint32_t nch = 0, avail = 0, r44 = 0;
+    if (L != 0) nch = round1_chunks<kLineP, kPolicy>(win, q0, L, avail, r44);
+    u32x4 v1[kWin1L];
+    load_round1<kLineP, ONC_DEC_COOP>(s_win, t, win, nch, v1);
     if (L != 0) {
-        nch = stage_window<kLine && kPolicy, kPolicy, kRoot>(s_win, t, base, win, q0, d0, L, needs2);
+        nch = stage_window<kLineP, kPolicy, kRoot>(s_win, t, base, win, q0, d0, L, needs2, v1, nch, avail, r44);
     }
     if constexpr (kPolicy) {
         // every 64th workgroup reports for the next launch how many of its
