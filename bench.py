@@ -93,6 +93,8 @@ def parse(argv=None):
     ap.add_argument("--cache-leg", choices=["on", "off"], default="on",
                     help="also measure the other cache state (c2: warm; c1: decode-only legs, warm and cold) and "
                          "report it next to the primary line")
+    ap.add_argument("--decode-policy", choices=["auto", "standard", "line"], default="auto",
+                    help="pin the decode's first-round policy for every codec of the run (A/B measurements)")
     ap.add_argument("--variant", type=lambda s: int(s, 0), default=0,
                     help="kernel variant bits (onc_codec_options.variant; A/B measurements only)")
     return ap.parse_args(argv)
@@ -1774,6 +1776,9 @@ def main():
 
     if args.variant:
         R.DEFAULT_OPTIONS["variant"] = args.variant     # A/B measurements: every codec of the run
+    if args.decode_policy != "auto":
+        R.DEFAULT_OPTIONS["decode_policy"] = {"standard": R.DECODE_POLICY_STANDARD,
+                                              "line": R.DECODE_POLICY_LINE}[args.decode_policy]
     dist = None
     torch.cuda.set_device(local_rank)
     if world > 1:
