@@ -378,3 +378,69 @@ def test_small_batch_lds_placement(codec, R, oracle, n):
         assert out[5:5 + total].cpu().numpy().tobytes() == o_wire
         assert np.array_equal(off.cpu().numpy().view(np.uint64), o_off)
         assert np.array_equal(st.cpu().numpy()[:hb.n], o_st)
+
+
+# ---------------------------------------------------------------------------
+# the decode's round 1 (decode.hip load_round1): cooperative buffer loads,
+# and the per-lane fallback when a wave's windows lie 2 GiB or more apart
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("policy", ["standard", "line"])
+@pytest.mark.parametrize("mode", [L.DECODE_SLICE, L.DECODE_BYTES])
+def test_decode_far_windows_fallback(R, oracle, policy, mode):
+    """Record 0 is a valid Call whose payload makes it 2 GiB - 200 bytes
+    long, so records 1-63 of its wave lie past the cooperative loader's
+    2 GiB resource and the wave takes the per-lane path: the oracle's
+    results, in both modes and policies. Records of the next waves (the
+    cooperative path) check the same way."""
+    import torch
+    big = (1 << 31) - 200
+    hb = S.mixed(200, seed=121, pmin=0, pmax=300, exotic=0.1)
+    ws, offs, st, _ = oracle.encode_batch(hb)
+    assert not st.any()
+    h0, _, _, _ = oracle.encode_batch(S.call_none(1, 0, seed=122))     # a Call with no payload
+    h0 = bytearray(h0)
+    h0[0:4] = ((big - 4) | 0x80000000).to_bytes(4, "big")             # its payload: the rest of 2 GiB
+    wire = np.zeros(big + len(ws) + 16, np.uint8)                      # zero pages: not touched
+    wire[:len(h0)] = np.frombuffer(bytes(h0), np.uint8)
+    wire[big:big + len(ws)] = np.frombuffer(ws, np.uint8)
+    off = np.concatenate([[0], big + offs.astype(np.uint64)]).astype(np.uint64)
+    pol = R.DECODE_POLICY_LINE if policy == "line" else R.DECODE_POLICY_STANDARD
+    c = R.Codec(0, decode_policy=pol)
+    try:
+        got = R.decode_host_wire(c, wire, off, mode)
+    finally:
+        c.close()
+    ora = oracle.decode_batch(wire, off, mode)
+    assert ora[2][0] == 0 and int(ora[0]["payload_len"][0]) == big - len(h0)
+    assert_decoded_equal(got, ora, f"far windows {policy}")
+    del wire
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("policy", ["standard", "line"])
+def test_decode_coop_short_and_empty_records(R, oracle, policy):
+    """Waves mixing empty records, records shorter than one granule,
+    records ending inside their first round and long headers, at odd
+    starts: the cooperative loader hands every lane its own granules (none
+    for an empty record), bit-exact against the oracle in both modes."""
+    recs = []
+    rng = np.random.default_rng(123)
+    hb = S.mixed(400, seed=124, pmin=0, pmax=64, exotic=0.3)
+    ws, offs, _, _ = oracle.encode_batch(hb)
+    full = [bytes(ws[int(offs[i]):int(offs[i + 1])]) for i in range(hb.n)]
+    for i in range(600):
+        k = rng.integers(0, 5)
+        r = full[i % hb.n]
+        recs.append(b"" if k == 0 else r[:int(rng.integers(1, 16))] if k == 1 else
+                    r[:int(rng.integers(16, 64))] if k == 2 else r)
+    wire, off = L.records_from_wire(recs)
+    w = np.concatenate([np.zeros(5, np.uint8), wire, np.zeros(16, np.uint8)])
+    off = off.astype(np.uint64) + 5                                    # every record start shifted by 5
+    pol = R.DECODE_POLICY_LINE if policy == "line" else R.DECODE_POLICY_STANDARD
+    c = R.Codec(0, decode_policy=pol)
+    try:
+        for mode in (L.DECODE_SLICE, L.DECODE_BYTES):
+            assert_decoded_equal(R.decode_host_wire(c, w, off, mode), oracle.decode_batch(w, off, mode),
+                                 f"coop {policy} mode {mode}")
+    finally:
+        c.close()
