@@ -12,6 +12,8 @@
   are counted, a range running past its pinned allocation is refused.
 * The one-launch small-batch encode after the single-pass lab's removal
   (placement through LDS only).
+* The decode's cooperative round 1 (decode.hip load_round1) on ragged
+  waves, and its per-lane fallback for windows 2 GiB apart.
 """
 import ctypes as C
 import mmap
