@@ -683,7 +683,11 @@ __device__ __forceinline__ uint32_t stage_window(uint32_t* s_win, int t, uintptr
         for (uint32_t j = 0; j < kN2; ++j) w[j] = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
         for (uint32_t j = kR2; j < kWinChunks; ++j)
+#if defined(ONC_LAB_NO_R2)
+            (void)0;                     // lab build only (wrong results): what round 2's loads cost
+#else
             if (j >= nch && j < want) w[j - kR2] = gload<u32x4>(win + 16 * j);
+#endif
         uint32_t f[4 * kN2 + 1];
 #pragma unroll
         for (uint32_t j = 0; j < kN2; ++j) {
