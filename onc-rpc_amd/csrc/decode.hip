@@ -33,6 +33,9 @@ namespace onc {
 #ifndef ONC_DEC_COOP
 #define ONC_DEC_COOP 1      // round 1 loaded cooperatively (load_round1)
 #endif
+#ifndef ONC_DEC_COOP2
+#define ONC_DEC_COOP2 1     // round 2 too, under the standard policy (load_round2_coop)
+#endif
 constexpr uint32_t kWin1 = 4;                 // round-1 chunks (standard policy)
 constexpr uint32_t kWin1L = 8;                // round-1 chunks at most (line policy, decode_kernel)
 constexpr uint32_t kWinChunks = ONC_DEC_WIN;
@@ -617,14 +620,23 @@ __device__ __forceinline__ void load_round1(uint32_t* s_win, int t, uintptr_t wi
     }
 }
 
+// Round 2 covers chunks [nch, want) from kR2 on (the first chunk round 1 may
+// have skipped) up to the window's end.
+template <bool kPolicy>
+struct Round2 {
+    static constexpr uint32_t kR2 = kPolicy ? 3u : kWin1;     // round 1 held >= 3 chunks if L >= 44
+    static constexpr uint32_t kN2 = kWinChunks > kR2 ? kWinChunks - kR2 : 1;
+};
+
 // The window of one record (L != 0), round 1 loaded (v, nch: load_round1):
-// staged, the header extent, round 2. Returns the chunks staged in LDS;
-// needs2: the header reaches past the standard policy's first round. kLine:
-// the line policy (decode_kernel).
+// round 1 staged in LDS and the header extent read from it. Returns the
+// chunks the header needs (want; > nch: round 2); needs2: the header
+// reaches past the standard policy's first round; last: round 1's last
+// word, whose upper bytes round 2 brings. kLine: the line policy.
 template <bool kLine, bool kPolicy, bool kRoot>
-__device__ __forceinline__ uint32_t stage_window(uint32_t* s_win, int t, uintptr_t base, uintptr_t win, uint32_t q0,
-                                                 uint32_t d0, uint64_t L, bool& needs2, const u32x4 (&v)[kWin1L],
-                                                 uint32_t nch, uint32_t avail, uint32_t r44) {
+__device__ __forceinline__ uint32_t stage_round1(uint32_t* s_win, int t, uintptr_t base, uint32_t q0, uint32_t d0,
+                                                 uint64_t L, bool& needs2, const u32x4 (&v)[kWin1L], uint32_t nch,
+                                                 uint32_t avail, uint32_t r44, uint32_t& last) {
     // column word c = record bytes [4c, 4c + 4): loaded words d0 + c and
     // d0 + c + 1 funnelled by the record's byte offset in its dword. The
     // last word of the round (its upper bytes in the next chunk) is
@@ -647,6 +659,10 @@ __device__ __forceinline__ uint32_t stage_window(uint32_t* s_win, int t, uintptr
         for (uint32_t r = 4 * kWin1; r < 4 * kWin1L; ++r)       // r >= 16 > d0
             if (r < 4 * nch) s_win[(r - d0) * kDecTile + t] = funnel(e[r], e[r + 1], sh);
     }
+    last = e[4 * kWin1L - 1];
+#pragma unroll
+    for (uint32_t c = 1; c < kWin1L; ++c)
+        if (nch == c) last = e[4 * c - 1];
     // Header extent from the first round: call -> 36 + cred body + verf
     // flavor/length + the verifier body (its length when the first round
     // holds it, else a 16-byte guess); reply -> up to 12 bytes past an
@@ -673,12 +689,88 @@ __device__ __forceinline__ uint32_t stage_window(uint32_t* s_win, int t, uintptr
     }
     const uint32_t want = min(avail, (q0 + need + 15) >> 4);
     needs2 = want > min(r44, avail);
-    if (want > nch) {
-        // chunks [nch, want): from kR2 on (the first chunk round 1 may
-        // have skipped) up to the window's end
-        constexpr uint32_t kR2 = kPolicy ? 3u : kWin1;   // round 1 held >= 3 chunks if L >= 44
-        constexpr uint32_t kN2 = kWinChunks > kR2 ? kWinChunks - kR2 : 1;
-        u32x4 w[kN2];
+    return want;
+}
+
+// Round 2's loads for the whole wave, cooperatively (the standard policy:
+// round 1 held 3 or 4 chunks, so a record's round 2 is at most 7): two
+// passes of 4 slots, lane t of instruction k taking slot t % 4 of record
+// 16 k + t / 4 — chunk nch + 4 p + slot when below want, else an
+// out-of-range offset (no request) — handed over through LDS rows [16, 32)
+// of the window (above round 1's staged rows). w[j - kR2] receives chunk j
+// of the lane's record for j in [nch, want), zeros elsewhere.
+template <bool kPolicy>
+__device__ __forceinline__ void load_round2_coop(uint32_t* s_win, int t, uintptr_t win, uint32_t nch, uint32_t want,
+                                                 u32x4 (&w)[Round2<kPolicy>::kN2]) {
+    constexpr uint32_t kR2 = Round2<kPolicy>::kR2, kN2 = Round2<kPolicy>::kN2;
+    static_assert(kR2 == 3 && kN2 == 7, "two passes of 4 slots cover round 2 after 3 or 4 round-1 chunks");
+#pragma unroll
+    for (uint32_t j = 0; j < kN2; ++j) w[j] = u32x4{0u, 0u, 0u, 0u};
+    const bool r2 = want > nch;
+    const uint64_t act = __ballot(r2);
+    if (act == 0) return;
+    const int first = __builtin_ctzll(act);
+    const uintptr_t rb = uintptr_t(__builtin_amdgcn_readlane(uint32_t(win), first)) |
+                         (uintptr_t(__builtin_amdgcn_readlane(uint32_t(win >> 32), first)) << 32);
+    const bool near = !r2 || (win >= rb && win - rb < (uintptr_t(1) << 31) - 256);
+    if (__ballot(!near) != 0) {                        // windows too far apart: per-lane loads
+#pragma unroll
+        for (uint32_t j = kR2; j < kWinChunks; ++j)
+            if (j >= nch && j < want) w[j - kR2] = gload<u32x4>(win + 16 * j);
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(rb), int16_t(0), int32_t(0x7FFFFFF0), int32_t(0x00020000));
+    const uint32_t wo = uint32_t(win - rb);
+    const uint32_t nw = r2 ? nch | (want << 8) : 0u;    // (nch, want) of the lane's record
+    const uint32_t slot = uint32_t(t) & 3u;
+    u32x4* raw = reinterpret_cast<u32x4*>(s_win + 16 * kDecTile);
+    u32x4 g[8];
+    const uint32_t passes = __ballot(r2 && want > nch + 4) ? 2u : 1u;   // wave-uniform
+#pragma unroll
+    for (uint32_t p = 0; p < 2; ++p) {
+        g[4 * p] = g[4 * p + 1] = g[4 * p + 2] = g[4 * p + 3] = u32x4{0u, 0u, 0u, 0u};
+        if (p < passes) {
+            u32x4 x[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const int r = int(16 * k + uint32_t(t) / 4);
+                const uint32_t wr = uint32_t(__shfl(int(wo), r));
+                const uint32_t q = uint32_t(__shfl(int(nw), r));
+                const uint32_t j = (q & 0xFFu) + 4 * p + slot;
+                x[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rs, j < (q >> 8) ? wr + 16 * j : 0x80000000u, 0, 0));
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) raw[4 * (16 * k + uint32_t(t) / 4) + slot] = x[k];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (uint32_t m = 0; m < 4; ++m) g[4 * p + m] = raw[4 * uint32_t(t) + m];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+    // slot m holds chunk nch + m: w[i] = chunk kR2 + i = slot i + kR2 - nch
+    // (nch is 3 or 4 for a record with a round 2)
+    if (r2) {
+#pragma unroll
+        for (uint32_t i = 0; i < kN2; ++i) w[i] = nch == kR2 ? g[i] : (i ? g[i - 1] : u32x4{0u, 0u, 0u, 0u});
+    }
+}
+
+// Round 2 of one record's window (want > nch): chunks [nch, want) staged
+// from w (loaded here when !kPre), and round 1's last word completed.
+// Returns the chunks staged (want).
+template <bool kPolicy, bool kPre>
+__device__ __forceinline__ uint32_t stage_round2(uint32_t* s_win, int t, uintptr_t win, uint32_t q0, uint32_t d0,
+                                                 uint32_t nch, uint32_t want, uint32_t last,
+                                                 u32x4 (&w)[Round2<kPolicy>::kN2]) {
+    constexpr uint32_t kR2 = Round2<kPolicy>::kR2, kN2 = Round2<kPolicy>::kN2;
+    const uint32_t sh = q0 & 3u;
+    if constexpr (!kPre) {
 #pragma unroll
         for (uint32_t j = 0; j < kN2; ++j) w[j] = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
@@ -688,31 +780,27 @@ __device__ __forceinline__ uint32_t stage_window(uint32_t* s_win, int t, uintptr
 #else
             if (j >= nch && j < want) w[j - kR2] = gload<u32x4>(win + 16 * j);
 #endif
-        uint32_t f[4 * kN2 + 1];
-#pragma unroll
-        for (uint32_t j = 0; j < kN2; ++j) {
-            f[4 * j] = w[j].x;
-            f[4 * j + 1] = w[j].y;
-            f[4 * j + 2] = w[j].z;
-            f[4 * j + 3] = w[j].w;
-        }
-        f[4 * kN2] = 0u;
-#pragma unroll
-        for (uint32_t r = 4 * kR2; r < 4 * kWinChunks; ++r)       // r >= 12 > d0
-            if (r >= 4 * nch && r < 4 * want) s_win[(r - d0) * kDecTile + t] = funnel(f[r - 4 * kR2], f[r - 4 * kR2 + 1], sh);
-        // round 1's last word, now with its upper bytes (nch >= kR2 here)
-        uint32_t lo = e[4 * kWin1L - 1], hi = w[0].x;
-#pragma unroll
-        for (uint32_t c = kR2; c < kWin1L; ++c)
-            if (nch == c) {
-                lo = e[4 * c - 1];
-                hi = w[c - kR2].x;
-            }
-        if (nch == kWin1L && kWin1L - kR2 < kN2) hi = w[kWin1L - kR2].x;
-        s_win[(4 * nch - 1 - d0) * kDecTile + t] = funnel(lo, hi, sh);
-        nch = want;
     }
-    return nch;
+    uint32_t f[4 * kN2 + 1];
+#pragma unroll
+    for (uint32_t j = 0; j < kN2; ++j) {
+        f[4 * j] = w[j].x;
+        f[4 * j + 1] = w[j].y;
+        f[4 * j + 2] = w[j].z;
+        f[4 * j + 3] = w[j].w;
+    }
+    f[4 * kN2] = 0u;
+#pragma unroll
+    for (uint32_t r = 4 * kR2; r < 4 * kWinChunks; ++r)       // r >= 12 > d0
+        if (r >= 4 * nch && r < 4 * want) s_win[(r - d0) * kDecTile + t] = funnel(f[r - 4 * kR2], f[r - 4 * kR2 + 1], sh);
+    // round 1's last word, now with its upper bytes (nch >= kR2 here)
+    uint32_t hi = w[0].x;
+#pragma unroll
+    for (uint32_t c = kR2; c < kWin1L; ++c)
+        if (nch == c) hi = w[c - kR2].x;
+    if (nch == kWin1L && kWin1L - kR2 < kN2) hi = w[kWin1L - kR2].x;
+    s_win[(4 * nch - 1 - d0) * kDecTile + t] = funnel(last, hi, sh);
+    return want;
 }
 
 template <int MODE, bool kExact = false, bool kNTOut = false, bool kFromLen = false, bool kBlkFused = false,
@@ -783,9 +871,14 @@ __global__ __launch_bounds__(kDecTile) void decode_kernel(DecArgs a) {
     if (L != 0) nch = round1_chunks<kLineP, kPolicy>(win, q0, L, avail, r44);
     u32x4 v1[kWin1L];
     load_round1<kLineP, ONC_DEC_COOP>(s_win, t, win, nch, v1);
-    if (L != 0) {
-        nch = stage_window<kLineP, kPolicy, kRoot>(s_win, t, base, win, q0, d0, L, needs2, v1, nch, avail, r44);
-    }
+    uint32_t want = 0, last = 0;
+    if (L != 0) want = stage_round1<kLineP, kPolicy, kRoot>(s_win, t, base, q0, d0, L, needs2, v1, nch, avail, r44, last);
+    // round 2 (headers longer than round 1): cooperative under the standard
+    // policy (the whole wave), else per lane
+    constexpr bool kCoop2 = ONC_DEC_COOP2 && kPolicy && !kLineP;
+    u32x4 w2[Round2<kPolicy>::kN2];
+    if constexpr (kCoop2) load_round2_coop<kPolicy>(s_win, t, win, nch, want, w2);
+    if (L != 0 && want > nch) nch = stage_round2<kPolicy, kCoop2>(s_win, t, win, q0, d0, nch, want, last, w2);
     if constexpr (kPolicy) {
         // every 64th workgroup reports for the next launch how many of its
         // records needed a second round under the standard policy
