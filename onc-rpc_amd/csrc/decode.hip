@@ -19,14 +19,16 @@
 
 namespace onc {
 
-// Each lane pulls the start of its record's 16-byte-aligned window into LDS
-// in two rounds of back-to-back dwordx4 loads (one memory latency per round
-// instead of one per field): first kWin1 chunks (64 B: the whole header of an
-// AUTH_NONE call), then, only for records whose header reaches further (the
-// credential length read from the first round), up to kWinChunks chunks
-// (160 B: an AUTH_UNIX call with 16 gids and a 16-byte machine name). The
-// window is laid out [word][lane] so that lanes parsing the same field hit
-// distinct banks. Reads past what was loaded fall back to global loads.
+// Each record's 16-byte-aligned window is pulled into LDS in two rounds of
+// dwordx4 loads (one memory latency per round instead of one per field):
+// first up to kWin1 chunks (64 B: the whole header of an AUTH_NONE call),
+// then, only for records whose header reaches further (the credential length
+// read from the first round), up to kWinChunks chunks (160 B: an AUTH_UNIX
+// call with 16 gids and a 16-byte machine name). The wave loads its records'
+// chunks cooperatively — lanes over a record's granules, handed over through
+// LDS (load_round1, load_round2_coop) — and each lane stages its own record.
+// The window is laid out [word][lane] so that lanes parsing the same field
+// hit distinct banks. Reads past what was loaded fall back to global loads.
 #ifndef ONC_DEC_WIN
 #define ONC_DEC_WIN 10
 #endif
@@ -562,6 +564,7 @@ template <bool kLine, bool kCoop>
 __device__ __forceinline__ void load_round1(uint32_t* s_win, int t, uintptr_t win, uint32_t nch, u32x4 (&v)[kWin1L]) {
     constexpr uint32_t G = kLine ? kWin1L : kWin1;
     static_assert(kWin1 == 4 && kWin1L == 8, "pin lists below");
+    static_assert(kDecTile == 64, "one wave per workgroup: the hand-over needs no workgroup barrier");
 #pragma unroll
     for (uint32_t j = 0; j < kWin1L; ++j) v[j] = u32x4{0u, 0u, 0u, 0u};
     const uint64_t act = __ballot(nch != 0);
