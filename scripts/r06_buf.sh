@@ -1,17 +1,17 @@
 #!/bin/bash
 # Round-6 A/B of the decode's window loads: the library against a lab build
-# B (default: tools/lab_buf1, -DONC_DEC_BUF2=0: round 2 with the per-lane
-# branches; the first A/B was against -DONC_DEC_BUF=0, the clamped round-1
-# re-reads): decode parity suites on the library first, then HBM-resident
-# steps (scripts/ab.sh) and the configs[2] zero-copy decode of a mapped wire
-# with each library.
+# B="name:dir" (a libonc_rpc_amd.so built into dir with one switch of
+# decode.hip turned off, e.g. -DONC_DEC_COOP2=0; the logs name each build):
+# decode parity suites on the library first (unless ZC_ONLY=1), then
+# HBM-resident steps (scripts/ab.sh) and the configs[2] zero-copy decode of a
+# mapped wire with each library.
 set -u
 mkdir -p gpurun_out
 [ "${ZC_ONLY:-0}" = 1 ] || {
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_decode_lengths.py tests/test_gpu_r04.py \
   tests/test_gpu_r05.py tests/test_body_roots.py -m gpu -x -q --timeout 200 --timeout-method thread \
   > gpurun_out/buf_tests.log 2>&1; r=$?; tail -2 gpurun_out/buf_tests.log; [ $r -eq 0 ] || exit $r
-B=${B:-buf1:tools/lab_buf1}
+B=${B:?set B=name:dir of the lab build}
 CASES="lib:onc-rpc_amd/libonc_rpc_amd.so:0 ${B%%:*}:${B#*:}/libonc_rpc_amd.so:0" WLS="c1 c2 c0 c3" ROUNDS=2 \
   bash scripts/ab.sh > gpurun_out/ab_buf.log 2>&1; r=$?; cat gpurun_out/ab_buf.log; [ $r -eq 0 ] || exit $r
 }
