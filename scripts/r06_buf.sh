@@ -7,11 +7,11 @@
 # mapped wire with each library.
 set -u
 mkdir -p gpurun_out
+B=${B:?set B=name:dir of the lab build}
 [ "${ZC_ONLY:-0}" = 1 ] || {
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_decode_lengths.py tests/test_gpu_r04.py \
   tests/test_gpu_r05.py tests/test_body_roots.py -m gpu -x -q --timeout 200 --timeout-method thread \
   > gpurun_out/buf_tests.log 2>&1; r=$?; tail -2 gpurun_out/buf_tests.log; [ $r -eq 0 ] || exit $r
-B=${B:?set B=name:dir of the lab build}
 CASES="lib:onc-rpc_amd/libonc_rpc_amd.so:0 ${B%%:*}:${B#*:}/libonc_rpc_amd.so:0" WLS="c1 c2 c0 c3" ROUNDS=2 \
   bash scripts/ab.sh > gpurun_out/ab_buf.log 2>&1; r=$?; cat gpurun_out/ab_buf.log; [ $r -eq 0 ] || exit $r
 }
